@@ -1,0 +1,327 @@
+#!/usr/bin/env python3
+"""Headline benchmark: batched CRC32C over device-resident 4 KiB SST blocks.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--nblocks B] [--e2e]
+
+Workload (BASELINE.json configs[1], "config 2"): per GPU, 16 Mi blocks x 4096 B
+(64 GiB) generated on the device from the splitmix64 stream, stride 4096,
+base 256-B aligned.  One step = one pass of the engine over the whole batch
+(leveldb_crc32c_batch_fixed, one persistent kernel launch) and, for N > 1, an
+RCCL gather of the 4-byte results to rank 0 (overlapped with the next pass on
+RCCL's own stream; the last one is inside the timed region).
+N > 1 runs one process per GPU under torch.distributed.run (weak scaling: each
+rank owns a different 64 GiB slice of the global block stream).
+
+Printed (rank 0): ONE JSON line with the driver's contract fields plus
+  roofline      dominant kernel vs the HBM roofline (HIP events on the launch stream)
+  cpu_baseline  the reference crc32c::Value (util/crc32c.cc compiled to
+                oracle/_ref/) on this host's cores over a bounded sample of the
+                same blocks, also cross-checked bit for bit against the GPU results
+  e2e           (with --e2e) host-resident rate incl. pinned H2D/D2H copies
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import glob
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "GiB/s CRC32C over device-resident 4 KiB SST blocks; bit-exact vs util/crc32c.cc"
+SEED = 0x5EED0001
+BLOCK = 4096
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+GIB = float(1 << 30)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--nblocks", type=int, default=1 << 24, help="4 KiB blocks per GPU")
+    ap.add_argument("--cpu-sample-blocks", type=int, default=1 << 18)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-seconds of reference work")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--e2e", action="store_true", help="also measure the host-resident (pinned copy) rate")
+    return ap.parse_args()
+
+
+def cpu_threads() -> int:
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit():
+        n = min(n, int(env))
+    return max(1, min(n, 16))
+
+
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline_leg(args, gpu_out) -> dict | None:
+    """Reference crc32c::Value timed on the host cores over the first
+    cpu_sample_blocks blocks of rank 0's shard; results compared with the GPU."""
+    import numpy as np
+
+    ref_so = os.path.join(ROOT, "oracle", "_ref", "libref_crc32c.so")
+    ora_so = os.path.join(ROOT, "oracle", "_build", "liboracle.so")
+    if not os.path.exists(ora_so):
+        return None
+    ora = ctypes.CDLL(ora_so)
+    ora.oracle_fill_synthetic.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_uint64]
+    nblk = min(args.cpu_sample_blocks, args.nblocks)
+    host = np.empty(nblk * BLOCK, dtype=np.uint8)
+    ora.oracle_fill_synthetic(host.ctypes.data, host.nbytes, SEED, 0)
+    out = np.empty(nblk, dtype=np.uint32)
+    threads = cpu_threads()
+    if os.path.exists(ref_so):
+        kind = "reference"
+        lib = ctypes.CDLL(ref_so)
+        lib.ref_crc32c_time_blocks.restype = ctypes.c_double
+        lib.ref_crc32c_time_blocks.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t,
+                                               ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+        accel = int(lib.ref_crc32c_accelerated())
+
+        def run(t, p):
+            return lib.ref_crc32c_time_blocks(host.ctypes.data, BLOCK, BLOCK, nblk, t, p, out.ctypes.data)
+    else:
+        kind = "port"
+        accel = 0
+        ora.oracle_crc32c_batch_fixed.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t,
+                                                  ctypes.c_size_t, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32]
+        threads = 1
+
+        def run(t, p):
+            t0 = time.perf_counter()
+            for _ in range(p):
+                ora.oracle_crc32c_batch_fixed(host.ctypes.data, BLOCK, BLOCK, nblk, 0, out.ctypes.data, 0)
+            return time.perf_counter() - t0
+
+    t1 = run(1, 1)  # single-thread calibration pass
+    rate1 = nblk * BLOCK / t1 / GIB
+    passes = max(1, int(round(args.cpu_seconds / max(t1, 1e-6) / threads)))
+    tn = run(threads, passes)
+    rate = nblk * BLOCK * passes / tn / GIB
+    g = gpu_out[:nblk].cpu().numpy().view(np.uint32)
+    agree = int((g == out).sum())
+    return {
+        "value": round(rate, 3), "unit": "GiB/s", "cores": threads, "kind": kind,
+        "sample": (f"crc32c::Value over the first {nblk} x 4096 B blocks of the same splitmix64 stream "
+                   f"(host-resident, {nblk * BLOCK / GIB:.2f} GiB), {passes} passes on {threads} threads "
+                   f"(~{tn * threads:.1f} CPU-s); 1 thread: {rate1:.3f} GiB/s"),
+        "single_thread_value": round(rate1, 3),
+        "path": "HAVE_CRC32C (libcrc32c)" if accel else "portable slicing-by-4 (util/crc32c.cc:276-377)",
+        "cpu_model": cpu_model(),
+        "agrees_with_gpu": f"{agree}/{nblk}",
+    }
+
+
+def load_pmc_traffic(nblocks: int):
+    """HBM bytes per launch of the span kernel from the committed PMC profile
+    (profiles/*pmc*.json, written by tools/pmc_summary.py), if it matches."""
+    best = None
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
+        try:
+            with open(p) as f:
+                d = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if d.get("nblocks") == nblocks and d.get("hbm_bytes_per_launch"):
+            best = d
+    return best
+
+
+def e2e_leg(args, torch, crc32c, dev) -> dict:
+    """Host-resident pipeline: pinned host blocks -> H2D -> CRC -> D2H, 3 streams
+    deep, chunks of 64 MiB (SST-file sized)."""
+    chunk_blocks = 16384  # 64 MiB = one 64 MiB SST's worth of 4 KiB blocks
+    nchunks = 48  # 3 GiB host-resident
+    depth = 3
+    host = torch.empty(chunk_blocks * BLOCK * 8, dtype=torch.uint8, pin_memory=True)  # 512 MiB pinned, reused
+    dbufs = [torch.empty(chunk_blocks * BLOCK, dtype=torch.uint8, device=dev) for _ in range(depth)]
+    douts = [torch.empty(chunk_blocks, dtype=torch.int32, device=dev) for _ in range(depth)]
+    houts = torch.empty(nchunks, chunk_blocks, dtype=torch.int32, pin_memory=True)
+    streams = [torch.cuda.Stream() for _ in range(depth)]
+    tmp = torch.empty(host.numel(), dtype=torch.uint8, device=dev)
+    crc32c.fill_synthetic(tmp, SEED)
+    host.copy_(tmp)
+    del tmp
+    torch.cuda.synchronize()
+
+    def run():
+        for c in range(nchunks):
+            s = streams[c % depth]
+            with torch.cuda.stream(s):
+                src = host[(c % 8) * chunk_blocks * BLOCK:((c % 8) + 1) * chunk_blocks * BLOCK]
+                dbufs[c % depth].copy_(src, non_blocking=True)
+                crc32c.batch_fixed(dbufs[c % depth], BLOCK, BLOCK, chunk_blocks, out=douts[c % depth])
+                houts[c].copy_(douts[c % depth], non_blocking=True)
+        torch.cuda.synchronize()
+
+    run()
+    t0 = time.perf_counter()
+    run()
+    t = time.perf_counter() - t0
+    # copy-only ceiling
+    t0 = time.perf_counter()
+    for c in range(nchunks):
+        with torch.cuda.stream(streams[c % depth]):
+            dbufs[c % depth].copy_(host[(c % 8) * chunk_blocks * BLOCK:((c % 8) + 1) * chunk_blocks * BLOCK],
+                                   non_blocking=True)
+    torch.cuda.synchronize()
+    tc = time.perf_counter() - t0
+    total = nchunks * chunk_blocks * BLOCK
+    return {"value": round(total / t / GIB, 2), "unit": "GiB/s", "copy_only_h2d": round(total / tc / GIB, 2),
+            "bytes": total, "pipeline": f"{depth} streams x 64 MiB chunks, pinned host, H2D->CRC->D2H"}
+
+
+def main() -> int:
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if rank == 0:
+            print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=dev)
+
+    from prismdb_amd import crc32c
+    from prismdb_amd.dist import ShardedBatch
+
+    crc32c.device_init(local)
+    nblk = args.nblocks
+    shard = ShardedBatch(nblocks_per_rank=nblk, block_bytes=BLOCK, rank=rank, world=world, device=dev)
+    buf = torch.empty(nblk * BLOCK, dtype=torch.uint8, device=dev)
+    crc32c.fill_synthetic(buf, SEED, byte_offset=shard.first_block * BLOCK)
+    outs = [torch.empty(nblk, dtype=torch.int32, device=dev) for _ in range(2)]
+    torch.cuda.synchronize()
+
+    stream = torch.cuda.current_stream()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    pending = [None, None]
+
+    def step(i, timed):
+        slot = i % 2
+        if pending[slot] is not None:
+            pending[slot].wait()  # the gather that still reads this output buffer
+            pending[slot] = None
+        if timed:
+            ev[i][0].record(stream)
+        crc32c.batch_fixed(buf, BLOCK, BLOCK, nblk, out=outs[slot])
+        if timed:
+            ev[i][1].record(stream)
+        if world > 1:
+            pending[slot] = shard.gather_async(outs[slot], slot)
+
+    for i in range(args.warmup):
+        step(i, False)
+    for w in pending:
+        if w is not None:
+            w.wait()
+    pending = [None, None]
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(i, True)
+    for w in pending:
+        if w is not None:
+            w.wait()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kern_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
+
+    t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed, kern_ms_max = float(t[0]), float(t[1])
+
+    total_bytes = world * nblk * BLOCK * args.steps
+    value = total_bytes / elapsed / GIB
+    algo_bytes = nblk * (BLOCK + 4)  # L read + 4 B result written per block
+    achieved = algo_bytes / (kern_ms / 1e3) / 1e9
+    # rank-0 results check: gathered results of the last step hold every rank's shard
+    gathered_ok = None
+    if world > 1:
+        gathered_ok = shard.check_gathered(outs[(args.steps - 1) % 2])
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline_leg(args, outs[(args.steps - 1) % 2])
+    e2e = e2e_leg(args, torch, crc32c, dev) if (args.e2e and rank == 0 and world == 1) else None
+
+    if rank == 0:
+        pmc = load_pmc_traffic(nblk)
+        line = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed * 1e3 / args.steps, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic (device-generated splitmix64 stream, regenerable on host)",
+            "config": {
+                "workload": "config2: 16Mi x 4096 B blocks per GPU, stride 4096, device-resident (BASELINE.json configs[1])"
+                if nblk == 1 << 24 else f"{nblk} x 4096 B blocks per GPU, stride 4096, device-resident",
+                "blocks_per_gpu": nblk,
+                "block_bytes": BLOCK,
+                "bytes_per_gpu": nblk * BLOCK,
+                "parallelism": f"shard{world}" + ("+rccl_gather" if world > 1 else ""),
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": pmc["hbm_bytes_per_launch"] if pmc else None,
+                "kernel": "crc32c_span_kernel<false,false>",
+                "kernel_ms": round(kern_ms, 4),
+                "kernel_ms_max_rank": round(kern_ms_max, 4),
+                "algorithmic_bytes_per_launch": algo_bytes,
+            },
+            "cpu_baseline": cpu,
+        }
+        if gathered_ok is not None:
+            line["gather_check"] = gathered_ok
+        if e2e is not None:
+            line["e2e_host_resident"] = e2e
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,94 @@
+/*
+ * prismdb_crc32c.h -- C ABI of the MI355X batched CRC32C engine.
+ *
+ * Drop-in boundary for LevelDB/PrismDB's block-checksum path.  Plain C types
+ * only (no HIP, no torch): device pointers are `const void*`, the stream is an
+ * opaque `void*` (a hipStream_t; NULL = the null stream).  Naming follows the
+ * reference's C API (include/leveldb/c.h: `leveldb_` prefix).
+ *
+ * Reference interfaces each entry point replaces or feeds:
+ *   leveldb_crc32c_extend/value   crc32c::Extend / Value          util/crc32c.h:17-20, util/crc32c.cc:276-377
+ *   leveldb_crc32c_mask/unmask    crc32c::Mask / Unmask           util/crc32c.h:27-38
+ *   leveldb_crc32c_batch*         N x crc32c::Value (+Extend type byte, +Mask) as issued by
+ *                                 TableBuilder::WriteRawBlock      table/table_builder.cc:185-202
+ *   ..._batch* with mismatch out  N x ReadBlock's verify          table/format.cc:91-102
+ *   leveldb_crc32c_accelerated    crc32c's CanAccelerateCRC32C    util/crc32c.cc:267-274
+ *                                 (port::AcceleratedCRC32C hook   port/port_stdcxx.h:141-151)
+ *
+ * Return convention: 0 = ok, < 0 = error (PRISMDB_CRC32C_E*); the message is in
+ * leveldb_crc32c_last_error() (thread-local).  A checksum MISMATCH is data, not
+ * an error: callers map mismatch[i] != 0 to Status::Corruption("block checksum
+ * mismatch") exactly as table/format.cc:99 does.
+ *
+ * Threading: every entry point is reentrant; concurrent calls on distinct
+ * streams take no lock after the one-time per-device initialisation.
+ * Ownership: the caller owns every buffer until the stream work completes; the
+ * engine keeps no pointer past the call.
+ */
+#ifndef PRISMDB_CRC32C_H_
+#define PRISMDB_CRC32C_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* flags */
+#define PRISMDB_CRC32C_MASK 0x1u /* out[i] = crc32c::Mask(crc)  (table/table_builder.cc:196) */
+
+/* error codes */
+#define PRISMDB_CRC32C_EINVAL (-1)  /* bad argument */
+#define PRISMDB_CRC32C_EDEVICE (-2) /* HIP runtime error */
+#define PRISMDB_CRC32C_ESELFTEST (-3) /* device known-answer self-test failed */
+
+/* ---- per-call host surface (CPU; per-call GPU launches would lose) ---- */
+
+/* crc32c::Extend (util/crc32c.cc:276): crc32c of A||data[0,n) given init_crc = crc32c(A). */
+uint32_t leveldb_crc32c_extend(uint32_t init_crc, const char* data, size_t n);
+/* crc32c::Value (util/crc32c.h:20) */
+uint32_t leveldb_crc32c_value(const char* data, size_t n);
+/* crc32c::Mask / Unmask (util/crc32c.h:27-38) */
+uint32_t leveldb_crc32c_mask(uint32_t crc);
+uint32_t leveldb_crc32c_unmask(uint32_t masked_crc);
+/* crc32c of A||B from crc32c(A), crc32c(B), |B| (no reference equivalent; used to stitch split spans). */
+uint32_t leveldb_crc32c_combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b);
+/* 1 if the host Extend uses the CPU's CRC32 instruction (KAT-gated like util/crc32c.cc:267-274). */
+int leveldb_crc32c_accelerated(void);
+
+/* ---- device batch surface (MI355X) ---- */
+
+/* One-time per-device setup (tables to HBM, device self-test against the
+ * util/crc32c.cc:269-273 vector).  Called implicitly by the batch functions;
+ * call it explicitly before stream capture. */
+int leveldb_crc32c_device_init(int device);
+
+/*
+ * Fixed-stride batch: block i = base[i*stride, i*stride + len), i < nblocks.
+ *   out[i]      = Extend(init, block_i)         (Mask()ed when flags & MASK)   -- may be NULL
+ *   mismatch[i] = Value(block_i) != Unmask(LE32(block_i + len))  (ReadBlock
+ *                 verify with len = n+1: contents||type, table/format.cc:93-95) -- may be NULL
+ * All pointers are device pointers on the current HIP device.
+ */
+int leveldb_crc32c_batch_fixed(const void* dev_base, size_t stride, size_t len, size_t nblocks,
+                               uint32_t init, uint32_t* dev_out, uint8_t* dev_mismatch,
+                               uint32_t flags, void* stream);
+
+/*
+ * Variable batch: block i = base[off[i], off[i] + len[i]); init[i] per block
+ * (dev_init may be NULL: all 0).  Any byte alignment, any length (< 4 GiB).
+ * Long spans are split across many wavefronts and recombined on the device.
+ */
+int leveldb_crc32c_batch(const void* dev_base, const uint64_t* dev_off, const uint32_t* dev_len,
+                         const uint32_t* dev_init, size_t n, uint32_t* dev_out,
+                         uint8_t* dev_mismatch, uint32_t flags, void* stream);
+
+/* Thread-local message for the last non-zero return on this thread. */
+const char* leveldb_crc32c_last_error(void);
+
+#ifdef __cplusplus
+} /* extern "C" */
+#endif
+
+#endif /* PRISMDB_CRC32C_H_ */

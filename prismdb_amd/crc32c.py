@@ -1,0 +1,146 @@
+"""Python face of leveldb::crc32c and of the MI355X batch engine.
+
+Per-call surface (same names/meaning as util/crc32c.h:17-38):
+    Extend(init_crc, data) -> int     crc32c(A || data) given init_crc = crc32c(A)
+    Value(data) -> int                crc32c(data)
+    Mask(crc) / Unmask(masked)        storage masking (rotate right 15 + kMaskDelta)
+These run on the host (a GPU launch per 4 KiB call would lose), through the
+native library's leveldb::crc32c::Extend.
+
+Batch surface (device-resident spans, one call = one batch of SST blocks):
+    batch_fixed(buf, stride, length, nblocks, ...)   block i = buf[i*stride : i*stride+length]
+    batch(buf, off, lens, init=None, ...)            span i  = buf[off[i] : off[i]+lens[i]]
+buf/off/lens/init/out are torch tensors on the current HIP device; calls are
+enqueued on torch's current stream.  mask=True applies Mask() to each result
+(TableBuilder::WriteRawBlock, table/table_builder.cc:194-196); verify=True also
+returns a per-span uint8 mismatch flag comparing Value(span) with
+Unmask(LE32(trailer at span end)) (ReadBlock, table/format.cc:91-102 with
+span = contents||type).  A mismatch is data: callers turn it into
+Status::Corruption("block checksum mismatch"), see prismdb_amd.sst.
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+from ._lib import check, lib
+
+kMaskDelta = 0xA282EAD8
+FLAG_MASK = 0x1
+
+
+def _bytes(data) -> bytes:
+    if isinstance(data, str):
+        return data.encode("latin-1")
+    return bytes(data)
+
+
+def Extend(init_crc: int, data) -> int:
+    b = _bytes(data)
+    return lib().leveldb_crc32c_extend(init_crc & 0xFFFFFFFF, b, len(b))
+
+
+def Value(data) -> int:
+    b = _bytes(data)
+    return lib().leveldb_crc32c_value(b, len(b))
+
+
+def Mask(crc: int) -> int:
+    return lib().leveldb_crc32c_mask(crc & 0xFFFFFFFF)
+
+
+def Unmask(masked_crc: int) -> int:
+    return lib().leveldb_crc32c_unmask(masked_crc & 0xFFFFFFFF)
+
+
+def Combine(crc_a: int, crc_b: int, len_b: int) -> int:
+    """crc32c(A || B) from crc32c(A), crc32c(B) and len(B)."""
+    return lib().leveldb_crc32c_combine(crc_a & 0xFFFFFFFF, crc_b & 0xFFFFFFFF, len_b)
+
+
+def accelerated() -> bool:
+    """True if the host Extend uses the CPU's CRC32 instruction (KAT-gated)."""
+    return bool(lib().leveldb_crc32c_accelerated())
+
+
+# ---------------------------------------------------------------- device batch
+
+
+def _torch():
+    import torch
+
+    return torch
+
+
+def _stream_ptr(stream) -> int:
+    torch = _torch()
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return int(s.cuda_stream)
+
+
+def device_init(device: int = 0) -> None:
+    check(lib().leveldb_crc32c_device_init(device), "leveldb_crc32c_device_init")
+
+
+def _require_device(*tensors):
+    for t in tensors:
+        if t is not None and not t.is_cuda:
+            raise ValueError("batch inputs must be device tensors (the engine has no CPU path)")
+
+
+def batch_fixed(buf, stride: int, length: int, nblocks: int, init: int = 0, *, mask: bool = False,
+                verify: bool = False, out=None, mismatch=None, stream=None) -> Tuple[object, Optional[object]]:
+    """CRC32C of nblocks fixed-stride blocks of a device buffer.
+
+    Returns (out uint32-as-int32 tensor [nblocks], mismatch uint8 [nblocks] or None).
+    """
+    torch = _torch()
+    _require_device(buf)
+    if nblocks and (nblocks - 1) * stride + length + (4 if verify else 0) > buf.numel() * buf.element_size():
+        raise ValueError("blocks extend past the end of buf")
+    if out is None:
+        out = torch.empty(nblocks, dtype=torch.int32, device=buf.device)
+    if verify and mismatch is None:
+        mismatch = torch.empty(nblocks, dtype=torch.uint8, device=buf.device)
+    rc = lib().leveldb_crc32c_batch_fixed(
+        buf.data_ptr(), stride, length, nblocks, init & 0xFFFFFFFF, out.data_ptr(),
+        mismatch.data_ptr() if verify else None, FLAG_MASK if mask else 0, _stream_ptr(stream))
+    check(rc, "leveldb_crc32c_batch_fixed")
+    return out, (mismatch if verify else None)
+
+
+def batch(buf, off, lens, init=None, *, mask: bool = False, verify: bool = False, out=None,
+          mismatch=None, stream=None) -> Tuple[object, Optional[object]]:
+    """CRC32C of arbitrary spans buf[off[i] : off[i]+lens[i]] (int64 off, int32 lens, int32 init)."""
+    torch = _torch()
+    _require_device(buf, off, lens, init)
+    n = off.numel()
+    if lens.numel() != n or (init is not None and init.numel() != n):
+        raise ValueError("off, lens and init must have the same length")
+    if off.dtype != torch.int64 or lens.dtype != torch.int32 or (init is not None and init.dtype != torch.int32):
+        raise TypeError("off must be int64, lens/init int32 (uint32 bit patterns)")
+    off, lens = off.contiguous(), lens.contiguous()
+    init = init.contiguous() if init is not None else None
+    if out is None:
+        out = torch.empty(n, dtype=torch.int32, device=buf.device)
+    if verify and mismatch is None:
+        mismatch = torch.empty(n, dtype=torch.uint8, device=buf.device)
+    rc = lib().leveldb_crc32c_batch(
+        buf.data_ptr(), off.data_ptr(), lens.data_ptr(), init.data_ptr() if init is not None else None, n,
+        out.data_ptr(), mismatch.data_ptr() if verify else None, FLAG_MASK if mask else 0,
+        _stream_ptr(stream))
+    check(rc, "leveldb_crc32c_batch")
+    return out, (mismatch if verify else None)
+
+
+def fill_synthetic(buf, seed: int, byte_offset: int = 0, stream=None) -> None:
+    """Fill a device buffer with the splitmix64 stream (see include/prismdb_synth.h)."""
+    _require_device(buf)
+    rc = lib().prismdb_fill_synthetic(buf.data_ptr(), buf.numel() * buf.element_size(), seed & (2**64 - 1),
+                                      byte_offset, _stream_ptr(stream))
+    if rc != 0:
+        raise RuntimeError(f"prismdb_fill_synthetic failed ({rc})")
+
+
+def as_u32(t):
+    """View an int32 result tensor as Python ints in [0, 2^32)."""
+    return [int(x) & 0xFFFFFFFF for x in t.tolist()]

@@ -1,0 +1,302 @@
+// crc32c_capi.hip -- C ABI of the batch engine (include/prismdb_crc32c.h).
+//
+// Per-device context (tables in HBM, CU count, self-test) is created once with
+// std::call_once; after that every call is lock-free.  The long-span split
+// path needs a small workspace; it is cached per (thread, device, stream) so
+// concurrent callers on distinct streams never share one.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <utility>
+
+#include "../../include/prismdb_crc32c.h"
+#include "crc32c_device.h"
+#include "crc32c_gf2.h"
+
+namespace {
+
+using prismdb::dev::DeviceTables;
+using prismdb::dev::SpanBatch;
+using prismdb::dev::SplitCounters;
+using prismdb::dev::SplitWs;
+
+thread_local std::string t_last_error;
+
+int Fail(int code, const std::string& msg) {
+  t_last_error = msg;
+  return code;
+}
+
+int FailHip(hipError_t e, const char* what) {
+  return Fail(PRISMDB_CRC32C_EDEVICE, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+constexpr int kMaxDevices = 64;
+
+struct DeviceCtx {
+  std::once_flag once;
+  int status = 0;
+  std::string error;
+  DeviceTables* tabs = nullptr;
+  int cus = 0;
+};
+
+DeviceCtx g_ctx[kMaxDevices];
+
+void BuildTables(DeviceTables* t) {
+  namespace g = prismdb::gf2;
+  g::StrideTables(prismdb::dev::kStrideBytes, t->stride);
+  for (int l = 0; l < 64; ++l) {
+    const g::Op m = g::ShiftBytes(prismdb::dev::kStrideBytes - 4u * (uint32_t)l);
+    for (int i = 0; i < 32; ++i) t->lane_mat[l][i] = m.col[i];
+  }
+  const g::Op s = g::ShiftBytes(prismdb::dev::kSegment);
+  for (int i = 0; i < 32; ++i) t->shift_seg[i] = s.col[i];
+}
+
+int RunBatch(DeviceCtx& ctx, const SpanBatch& base_args, bool desc, bool verify, hipStream_t s);
+
+// Device known-answer self-test (util/crc32c.cc:269-273 vector, plus a 4 KiB
+// block and a > kLongSpan span checked against the host Extend).
+int SelfTest(DeviceCtx& ctx) {
+  const size_t kBig = prismdb::dev::kLongSpan + 3 * prismdb::dev::kSegment + 77;
+  const size_t bytes = 64 + 4096 + kBig;
+  unsigned char* h = new unsigned char[bytes];
+  std::memset(h, 0, 64);
+  std::memcpy(h + 1, "TestCRCBuffer", 13);
+  uint64_t z = 0x5EED0001ull;
+  for (size_t i = 64; i < bytes; ++i) {
+    z = z * 6364136223846793005ull + 1442695040888963407ull;
+    h[i] = (unsigned char)(z >> 56);
+  }
+  const uint64_t off[3] = {1, 64, 64 + 4096};
+  const uint32_t len[3] = {13, 4096, (uint32_t)kBig};
+  const uint32_t want[3] = {0xdcbc59fau,
+                            leveldb_crc32c_value(reinterpret_cast<const char*>(h) + 64, 4096),
+                            leveldb_crc32c_value(reinterpret_cast<const char*>(h) + 64 + 4096, kBig)};
+  unsigned char* d = nullptr;
+  hipError_t e = hipMalloc(&d, bytes + 3 * 8 + 3 * 4 + 3 * 4);
+  if (e != hipSuccess) {
+    delete[] h;
+    return FailHip(e, "self-test hipMalloc");
+  }
+  uint64_t* d_off = reinterpret_cast<uint64_t*>(d + ((bytes + 7) & ~size_t(7)));
+  uint32_t* d_len = reinterpret_cast<uint32_t*>(d_off + 3);
+  uint32_t* d_out = d_len + 3;
+  hipMemcpy(d, h, bytes, hipMemcpyHostToDevice);
+  hipMemcpy(d_off, off, sizeof(off), hipMemcpyHostToDevice);
+  hipMemcpy(d_len, len, sizeof(len), hipMemcpyHostToDevice);
+  SpanBatch a{};
+  a.base = d;
+  a.off = d_off;
+  a.len = d_len;
+  a.n = 3;
+  a.out = d_out;
+  int rc = RunBatch(ctx, a, true, false, nullptr);
+  uint32_t got[3] = {0, 0, 0};
+  if (rc == 0) {
+    e = hipStreamSynchronize(nullptr);
+    if (e != hipSuccess) rc = FailHip(e, "self-test sync");
+  }
+  if (rc == 0) hipMemcpy(got, d_out, sizeof(got), hipMemcpyDeviceToHost);
+  hipFree(d);
+  delete[] h;
+  if (rc != 0) return rc;
+  for (int i = 0; i < 3; ++i) {
+    if (got[i] != want[i]) {
+      char buf[160];
+      std::snprintf(buf, sizeof(buf), "device self-test %d: got %08x want %08x", i, got[i], want[i]);
+      return Fail(PRISMDB_CRC32C_ESELFTEST, buf);
+    }
+  }
+  return 0;
+}
+
+void InitDevice(DeviceCtx& ctx, int device) {
+  hipError_t e = hipDeviceGetAttribute(&ctx.cus, hipDeviceAttributeMultiprocessorCount, device);
+  if (e != hipSuccess || ctx.cus <= 0) {
+    ctx.status = FailHip(e, "hipDeviceGetAttribute(multiprocessor count)");
+    ctx.error = t_last_error;
+    return;
+  }
+  DeviceTables* host = new DeviceTables;
+  BuildTables(host);
+  e = hipMalloc(&ctx.tabs, sizeof(DeviceTables));
+  if (e == hipSuccess) e = hipMemcpy(ctx.tabs, host, sizeof(DeviceTables), hipMemcpyHostToDevice);
+  delete host;
+  if (e != hipSuccess) {
+    ctx.status = FailHip(e, "table upload");
+    ctx.error = t_last_error;
+    return;
+  }
+  ctx.status = SelfTest(ctx);
+  if (ctx.status != 0) ctx.error = t_last_error;
+}
+
+int GetCtx(DeviceCtx** out) {
+  int device = 0;
+  hipError_t e = hipGetDevice(&device);
+  if (e != hipSuccess) return FailHip(e, "hipGetDevice");
+  if (device < 0 || device >= kMaxDevices) return Fail(PRISMDB_CRC32C_EINVAL, "device ordinal out of range");
+  DeviceCtx& ctx = g_ctx[device];
+  std::call_once(ctx.once, [&]() { InitDevice(ctx, device); });
+  if (ctx.status != 0) return Fail(ctx.status, ctx.error);
+  *out = &ctx;
+  return 0;
+}
+
+// ---- split-path workspace, per (thread, device, stream) ----
+struct Workspace {
+  void* mem = nullptr;
+  SplitWs ws{};
+};
+
+constexpr uint64_t kCapSeg = 1u << 20;   // 1 Mi segments = 32 GiB of long spans per call
+constexpr uint32_t kCapLong = 1u << 18;
+
+int GetWorkspace(hipStream_t s, SplitWs* out) {
+  thread_local std::map<std::pair<int, hipStream_t>, Workspace> cache;
+  int device = 0;
+  hipGetDevice(&device);
+  Workspace& w = cache[{device, s}];
+  if (w.mem == nullptr) {
+    const size_t bytes = 256 + kCapSeg * (8 + 4 + 4 + 4) + (size_t)kCapLong * (8 + 8 + 4);
+    hipError_t e = hipMalloc(&w.mem, bytes);
+    if (e != hipSuccess) {
+      w.mem = nullptr;
+      return FailHip(e, "split workspace hipMalloc");
+    }
+    char* p = static_cast<char*>(w.mem);
+    w.ws.counters = reinterpret_cast<SplitCounters*>(p);
+    p += 256;
+    w.ws.seg_off = reinterpret_cast<uint64_t*>(p);
+    p += kCapSeg * 8;
+    w.ws.long_span = reinterpret_cast<uint64_t*>(p);
+    p += (size_t)kCapLong * 8;
+    w.ws.long_first = reinterpret_cast<uint64_t*>(p);
+    p += (size_t)kCapLong * 8;
+    w.ws.seg_len = reinterpret_cast<uint32_t*>(p);
+    p += kCapSeg * 4;
+    w.ws.seg_init = reinterpret_cast<uint32_t*>(p);
+    p += kCapSeg * 4;
+    w.ws.seg_out = reinterpret_cast<uint32_t*>(p);
+    p += kCapSeg * 4;
+    w.ws.long_nseg = reinterpret_cast<uint32_t*>(p);
+    w.ws.cap_seg = kCapSeg;
+    w.ws.cap_long = kCapLong;
+  }
+  *out = w.ws;
+  return 0;
+}
+
+// Launch sequence.  Spans that may exceed kLongSpan go through
+// plan -> span pass (long spans skipped) -> segment pass -> combine.
+int RunBatch(DeviceCtx& ctx, const SpanBatch& base_args, bool desc, bool verify, hipStream_t s) {
+  SpanBatch a = base_args;
+  a.tabs = ctx.tabs;
+  a.role = prismdb::dev::kRoleSpans;
+  const bool may_be_long = desc || a.len_c > prismdb::dev::kLongSpan;
+  if (!may_be_long) {
+    a.skip_above = 0xFFFFFFFFu;
+    a.overflow = nullptr;
+    hipError_t e = prismdb::dev::launch_span(a, desc, verify, ctx.cus, s);
+    return e == hipSuccess ? 0 : FailHip(e, "span kernel launch");
+  }
+  SplitWs ws{};
+  int rc = GetWorkspace(s, &ws);
+  if (rc != 0) return rc;
+  hipError_t e = hipMemsetAsync(ws.counters, 0, sizeof(SplitCounters), s);
+  if (e != hipSuccess) return FailHip(e, "hipMemsetAsync");
+  a.skip_above = prismdb::dev::kLongSpan;
+  a.overflow = &ws.counters->overflow;
+  e = prismdb::dev::launch_plan(a, desc, ws, s);
+  if (e != hipSuccess) return FailHip(e, "plan kernel launch");
+  e = prismdb::dev::launch_span(a, desc, verify, ctx.cus, s);
+  if (e != hipSuccess) return FailHip(e, "span kernel launch");
+  SpanBatch seg{};
+  seg.base = a.base;
+  seg.off = ws.seg_off;
+  seg.len = ws.seg_len;
+  seg.init = ws.seg_init;
+  seg.n = ws.cap_seg;
+  seg.n_dev = &ws.counters->nseg;
+  seg.out = ws.seg_out;
+  seg.skip_above = 0xFFFFFFFFu;
+  seg.overflow = &ws.counters->overflow;
+  seg.role = prismdb::dev::kRoleSegments;
+  seg.tabs = ctx.tabs;
+  e = prismdb::dev::launch_span(seg, true, false, ctx.cus, s);
+  if (e != hipSuccess) return FailHip(e, "segment kernel launch");
+  e = prismdb::dev::launch_combine(a, desc, verify, ws, s);
+  return e == hipSuccess ? 0 : FailHip(e, "combine kernel launch");
+}
+
+}  // namespace
+
+extern "C" {
+
+int leveldb_crc32c_device_init(int device) {
+  int cur = 0;
+  hipError_t e = hipGetDevice(&cur);
+  if (e != hipSuccess) return FailHip(e, "hipGetDevice");
+  if (device != cur) {
+    e = hipSetDevice(device);
+    if (e != hipSuccess) return FailHip(e, "hipSetDevice");
+  }
+  DeviceCtx* ctx = nullptr;
+  int rc = GetCtx(&ctx);
+  if (device != cur) hipSetDevice(cur);
+  return rc;
+}
+
+int leveldb_crc32c_batch_fixed(const void* dev_base, size_t stride, size_t len, size_t nblocks,
+                               uint32_t init, uint32_t* dev_out, uint8_t* dev_mismatch,
+                               uint32_t flags, void* stream) {
+  if (nblocks == 0) return 0;
+  if (dev_base == nullptr) return Fail(PRISMDB_CRC32C_EINVAL, "dev_base is NULL");
+  if (len > 0xFFFFFFFFull) return Fail(PRISMDB_CRC32C_EINVAL, "len must be < 4 GiB");
+  if ((flags & ~PRISMDB_CRC32C_MASK) != 0) return Fail(PRISMDB_CRC32C_EINVAL, "unknown flag bits");
+  DeviceCtx* ctx = nullptr;
+  int rc = GetCtx(&ctx);
+  if (rc != 0) return rc;
+  SpanBatch a{};
+  a.base = static_cast<const uint8_t*>(dev_base);
+  a.stride = stride;
+  a.len_c = (uint32_t)len;
+  a.init_c = init;
+  a.n = nblocks;
+  a.out = dev_out;
+  a.mismatch = dev_mismatch;
+  a.flags = flags;
+  return RunBatch(*ctx, a, false, dev_mismatch != nullptr, static_cast<hipStream_t>(stream));
+}
+
+int leveldb_crc32c_batch(const void* dev_base, const uint64_t* dev_off, const uint32_t* dev_len,
+                         const uint32_t* dev_init, size_t n, uint32_t* dev_out,
+                         uint8_t* dev_mismatch, uint32_t flags, void* stream) {
+  if (n == 0) return 0;
+  if (dev_base == nullptr || dev_off == nullptr || dev_len == nullptr)
+    return Fail(PRISMDB_CRC32C_EINVAL, "dev_base/dev_off/dev_len must be non-NULL");
+  if ((flags & ~PRISMDB_CRC32C_MASK) != 0) return Fail(PRISMDB_CRC32C_EINVAL, "unknown flag bits");
+  DeviceCtx* ctx = nullptr;
+  int rc = GetCtx(&ctx);
+  if (rc != 0) return rc;
+  SpanBatch a{};
+  a.base = static_cast<const uint8_t*>(dev_base);
+  a.off = dev_off;
+  a.len = dev_len;
+  a.init = dev_init;
+  a.n = n;
+  a.out = dev_out;
+  a.mismatch = dev_mismatch;
+  a.flags = flags;
+  return RunBatch(*ctx, a, true, dev_mismatch != nullptr, static_cast<hipStream_t>(stream));
+}
+
+const char* leveldb_crc32c_last_error(void) { return t_last_error.c_str(); }
+
+}  // extern "C"

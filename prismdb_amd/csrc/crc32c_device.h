@@ -1,0 +1,80 @@
+// crc32c_device.h -- shared between the HIP kernels and the C-ABI host code.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace prismdb {
+namespace dev {
+
+constexpr uint32_t kPolyReflected = 0x82F63B78u;
+constexpr uint32_t kConditioning = 0xFFFFFFFFu;  // util/crc32c.cc:246
+constexpr uint32_t kMaskDelta = 0xa282ead8u;     // util/crc32c.h:22
+constexpr uint32_t kFlagMask = 0x1u;             // == PRISMDB_CRC32C_MASK
+
+constexpr int kWave = 64;
+constexpr int kWavesPerGroup = 16;                 // 1024-thread workgroup, one per CU
+constexpr int kThreads = kWave * kWavesPerGroup;
+constexpr int kRounds = 16;                        // 256-B rounds per chunk
+constexpr uint32_t kChunkWords = kRounds * kWave;  // 1024 words = 4 KiB per chunk
+constexpr uint32_t kStrideBytes = 4u * kWave;      // 256 B between a lane's words
+constexpr int kCopies = 32;                        // LDS table replication (bank = lane % 32)
+constexpr int kTabWords = 4 * 256 * kCopies;       // 128 KiB of LDS
+
+constexpr uint32_t kLongSpan = 128u * 1024u;       // spans above this are split...
+constexpr uint32_t kSegment = 32u * 1024u;         // ...into pieces of this size
+
+// Tables derived on the host from the polynomial (crc32c_gf2.h) and kept in HBM.
+struct DeviceTables {
+  uint32_t stride[4][256];    // stride[k][b] = shift_256(b << 8k)
+  uint32_t lane_mat[64][32];  // column i of shift_{256-4l} for lane l
+  uint32_t shift_seg[32];     // column i of shift_kSegment
+};
+
+enum : uint32_t { kRoleSpans = 0, kRoleSegments = 1 };
+
+struct SpanBatch {
+  const uint8_t* base;
+  const uint64_t* off;   // descriptor mode
+  const uint32_t* len;
+  const uint32_t* init;  // nullable
+  uint64_t stride;       // fixed mode
+  uint32_t len_c;
+  uint32_t init_c;
+  uint64_t n;
+  const unsigned long long* n_dev;  // nullable: n = min(n, *n_dev)
+  uint32_t* out;                    // nullable
+  uint8_t* mismatch;                // nullable (verify)
+  uint32_t flags;
+  uint32_t skip_above;              // spans longer than this are left to the split path
+  const uint32_t* overflow;         // nullable: split-path overflow flag
+  uint32_t role;
+  const DeviceTables* tabs;
+};
+
+struct SplitCounters {
+  unsigned long long nseg;
+  uint32_t nlong;
+  uint32_t overflow;
+};
+
+struct SplitWs {
+  SplitCounters* counters;
+  uint64_t* seg_off;
+  uint32_t* seg_len;
+  uint32_t* seg_init;
+  uint32_t* seg_out;
+  uint64_t* long_span;
+  uint64_t* long_first;
+  uint32_t* long_nseg;
+  uint64_t cap_seg;
+  uint32_t cap_long;
+};
+
+hipError_t launch_span(const SpanBatch& a, bool desc, bool verify, int grid, hipStream_t s);
+hipError_t launch_plan(const SpanBatch& a, bool desc, const SplitWs& ws, hipStream_t s);
+hipError_t launch_combine(const SpanBatch& a, bool desc, bool verify, const SplitWs& ws,
+                          hipStream_t s);
+
+}  // namespace dev
+}  // namespace prismdb

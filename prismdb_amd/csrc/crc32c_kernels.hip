@@ -1,0 +1,410 @@
+// crc32c_kernels.hip -- CDNA4 (gfx950) kernels of the batched CRC32C engine.
+//
+// What is computed: for every span i, crc32c::Extend(init_i, base+off_i, len_i)
+// (util/crc32c.cc:276-377), optionally Mask()ed (util/crc32c.h:27-31, as
+// TableBuilder::WriteRawBlock stores it, table/table_builder.cc:194-196) and/or
+// compared against the stored trailer (ReadBlock verify, table/format.cc:93-95).
+//
+// How (one span per 64-lane wavefront, HBM-bound design):
+//   * The span is cut into head bytes (to 4-B alignment), W body words and
+//     tail bytes.  Body word i goes to lane (i - W) mod 64: the wave reads 256
+//     contiguous bytes per round (coalesced dword loads), rounds right-aligned
+//     so that every lane's last word is in the final round.
+//   * Each lane runs its own CRC stream with stride 256 B:
+//         acc <- shift_256(acc) ^ word
+//     where shift_256 (register advanced over 256 zero bytes) is four lookups
+//     in LDS stride tables.  The tables are replicated 32x, interleaved so
+//     that lane l always reads bank (l mod 32): ds_read_b32 never conflicts.
+//   * Lane l's stream ends 256-4l bytes before the body end, so its partial is
+//     moved there by a per-lane 32x32 GF(2) matrix held in 32 VGPRs
+//     (shift_{256-4l}), then the wave XOR-reduces with DPP.  The span's initial
+//     register (init, head bytes) is injected into body word 0.
+//   * Persistent grid (one 1024-thread workgroup per CU: the 128 KiB of LDS
+//     tables are loaded once per CU), spans dealt round-robin to waves, next
+//     chunk's loads issued before the current chunk is folded (register double
+//     buffer), descriptors staged 64 spans at a time in lanes.
+//   * Spans longer than kLongSpan are cut into kSegment pieces by a planner
+//     kernel, processed as independent spans, then stitched with the constant
+//     operator shift_kSegment (CRC combination) by a combine kernel.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "crc32c_device.h"
+
+namespace prismdb {
+namespace dev {
+
+namespace {
+
+__device__ __forceinline__ uint32_t rfl(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ uint32_t readlane(uint32_t x, uint32_t l) {
+  return __builtin_amdgcn_readlane(x, l);
+}
+
+// XOR of v over the 64 lanes (wave-uniform result).
+__device__ __forceinline__ uint32_t wave_xor(uint32_t v) {
+  v ^= __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+  v ^= __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+  v ^= __builtin_amdgcn_mov_dpp(v, 0x141, 0xF, 0xF, false);  // row_half_mirror
+  v ^= __builtin_amdgcn_mov_dpp(v, 0x140, 0xF, 0xF, false);  // row_mirror
+  return readlane(v, 0) ^ readlane(v, 16) ^ readlane(v, 32) ^ readlane(v, 48);
+}
+
+// One zero byte through the reflected LFSR, bit-serial (wave-uniform, SALU).
+__device__ __forceinline__ uint32_t feed_byte(uint32_t r, uint32_t byte) {
+  r ^= byte;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) r = (r >> 1) ^ (kPolyReflected & (0u - (r & 1u)));
+  return r;
+}
+
+__device__ __forceinline__ uint32_t mask_crc(uint32_t c) { return ((c << 17) | (c >> 15)) + kMaskDelta; }
+__device__ __forceinline__ uint32_t unmask_crc(uint32_t m) {
+  const uint32_t r = m - kMaskDelta;
+  return (r << 15) | (r >> 17);
+}
+
+// Wave-uniform description of one span.
+struct Geo {
+  const uint8_t* p;  // first byte
+  uint32_t len, init;
+  uint32_t h;        // head bytes (to 4-byte alignment), 0..3
+  uint32_t W;        // body words
+  uint32_t t;        // tail bytes, 0..3
+  uint32_t nch;      // chunks of kChunkWords body words (>= 1)
+  uint32_t pad;      // nch*kChunkWords - W: leading zero words of chunk 0
+  bool skip;         // handled by the long-span path instead
+};
+
+__device__ __forceinline__ Geo make_geo(const uint8_t* p, uint32_t len, uint32_t init, bool skip) {
+  Geo g;
+  g.p = p;
+  g.len = len;
+  g.init = init;
+  uint32_t h = (4u - ((uint32_t)(uintptr_t)p & 3u)) & 3u;
+  if (h > len) h = len;
+  g.h = h;
+  g.W = (len - h) >> 2;
+  g.t = (len - h) & 3u;
+  g.nch = g.W ? (g.W + kChunkWords - 1u) / kChunkWords : 1u;
+  g.pad = g.nch * kChunkWords - g.W;
+  g.skip = skip;
+  return g;
+}
+
+// shift_256(acc): four LDS lookups, lane-private bank (see header comment).
+__device__ __forceinline__ uint32_t shift256(const uint32_t* __restrict__ tab, uint32_t acc) {
+  const uint32_t a0 = tab[(acc & 0xffu) << 5];
+  const uint32_t a1 = tab[(1u << 13) + (((acc >> 8) & 0xffu) << 5)];
+  const uint32_t a2 = tab[(2u << 13) + (((acc >> 16) & 0xffu) << 5)];
+  const uint32_t a3 = tab[(3u << 13) + ((acc >> 24) << 5)];
+  return a0 ^ a1 ^ a2 ^ a3;
+}
+
+// Issue the body loads of chunk c of g into w[] (no wait).
+__device__ __forceinline__ void issue_chunk(const Geo& g, uint32_t c, uint32_t lane,
+                                            uint32_t (&w)[kRounds]) {
+  const uint32_t* body = reinterpret_cast<const uint32_t*>(g.p + g.h);
+  const int32_t i0 = (int32_t)(c * kChunkWords + lane) - (int32_t)g.pad;
+  if (c == 0 && g.pad != 0) {
+#pragma unroll
+    for (int j = 0; j < kRounds; ++j) {
+      const int32_t i = i0 + 64 * j;
+      w[j] = __builtin_nontemporal_load(body + (i < 0 ? 0 : i));
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < kRounds; ++j) w[j] = __builtin_nontemporal_load(body + i0 + 64 * j);
+  }
+}
+
+// Issue the edge-byte load of a span: lanes 0..h-1 head, 3..3+t-1 tail,
+// 6..9 stored trailer (verify).
+template <bool kVerify>
+__device__ __forceinline__ uint32_t issue_edges(const Geo& g, uint32_t lane) {
+  const uint8_t* src = nullptr;
+  if (lane < g.h)
+    src = g.p + lane;
+  else if (lane >= 3u && lane < 3u + g.t)
+    src = g.p + g.h + 4ull * g.W + (lane - 3u);
+  else if (kVerify && lane >= 6u && lane < 10u)
+    src = g.p + g.len + (lane - 6u);
+  uint32_t e = 0;
+  if (src != nullptr) e = *src;
+  return e;
+}
+
+struct Desc {
+  uint32_t off_lo, off_hi, len, init;
+};
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// Main span kernel.
+// ---------------------------------------------------------------------------
+template <bool kDesc, bool kVerify>
+__global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
+  uint64_t n = a.n;
+  if (a.n_dev != nullptr) {
+    const uint64_t m = *a.n_dev;
+    n = m < n ? m : n;
+  }
+  uint32_t skip_above = a.skip_above;
+  if (a.overflow != nullptr && *a.overflow != 0u) {
+    if (a.role == kRoleSegments) n = 0;   // split path abandoned: nothing to do
+    else skip_above = 0xFFFFFFFFu;        // ...and the span pass takes every span whole
+  }
+  if (n == 0) return;
+
+  __shared__ uint32_t lds[kTabWords];
+  const uint32_t tid = threadIdx.x;
+  {
+    const uint32_t* src = &a.tabs->stride[0][0];
+    for (uint32_t e = tid; e < (uint32_t)kTabWords; e += kThreads) lds[e] = src[e >> 5];
+  }
+  const uint32_t lane = tid & 63u;
+  uint32_t M[32];
+#pragma unroll
+  for (int i = 0; i < 32; ++i) M[i] = a.tabs->lane_mat[lane][i];
+  __syncthreads();
+
+  const uint32_t* tab = lds + (lane & 31u);
+  const uint64_t wave = rfl(blockIdx.x * kWavesPerGroup + (tid >> 6));
+  const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerGroup;
+  if (wave >= n) return;
+
+  // --- descriptor staging (variable batches): lane q holds span k = 64*G + q ---
+  Desc dcur{0, 0, 0, 0}, dnx{0, 0, 0, 0};
+  auto load_desc = [&](uint64_t group) -> Desc {
+    Desc d{0, 0, 0, 0};
+    const uint64_t b = wave + (group * 64u + lane) * nwaves;
+    if (b < n) {
+      const uint64_t o = a.off[b];
+      d.off_lo = (uint32_t)o;
+      d.off_hi = (uint32_t)(o >> 32);
+      d.len = a.len[b];
+      d.init = a.init != nullptr ? a.init[b] : 0u;
+    }
+    return d;
+  };
+  auto geo_of = [&](uint64_t k) -> Geo {
+    const uint64_t b = wave + k * nwaves;
+    uint64_t off;
+    uint32_t len, init;
+    if (kDesc) {
+      const uint32_t q = (uint32_t)(k & 63u);
+      off = ((uint64_t)readlane(dcur.off_hi, q) << 32) | readlane(dcur.off_lo, q);
+      len = readlane(dcur.len, q);
+      init = readlane(dcur.init, q);
+    } else {
+      off = b * a.stride;
+      len = a.len_c;
+      init = a.init_c;
+    }
+    return make_geo(a.base + off, len, init, len > skip_above);
+  };
+  if (kDesc) {
+    dcur = load_desc(0);
+    dnx = load_desc(1);
+  }
+
+  uint64_t k = 0;  // span ordinal within this wave
+  uint32_t c = 0;  // chunk within the span
+  Geo g = geo_of(0);
+  uint32_t nx[kRounds];
+  uint32_t enx = 0;
+  if (!g.skip) {
+    if (g.W) issue_chunk(g, 0, lane, nx);
+    if (g.h | g.t | (uint32_t)kVerify) enx = issue_edges<kVerify>(g, lane);
+  }
+
+  uint32_t r = 0, acc = 0, ecur = 0;
+  while (true) {
+    uint32_t cur[kRounds];
+#pragma unroll
+    for (int j = 0; j < kRounds; ++j) cur[j] = nx[j];
+    if (c == 0) ecur = enx;
+
+    // -- next task and its loads (issued before this chunk is folded) --
+    uint64_t k2 = k;
+    uint32_t c2 = c + 1;
+    if (c2 == g.nch) {
+      k2 = k + 1;
+      c2 = 0;
+    }
+    const bool have_next = wave + k2 * nwaves < n;
+    Geo g2 = g;
+    if (have_next) {
+      if (c2 == 0) {
+        if (kDesc && (k2 & 63u) == 0) {
+          dcur = dnx;
+          dnx = load_desc((k2 >> 6) + 1);
+        }
+        g2 = geo_of(k2);
+      }
+      if (!g2.skip) {
+        if (g2.W) issue_chunk(g2, c2, lane, nx);
+        if (c2 == 0 && (g2.h | g2.t | (uint32_t)kVerify)) enx = issue_edges<kVerify>(g2, lane);
+      }
+    }
+
+    if (!g.skip) {
+      // -- span start: initial register through the head bytes --
+      if (c == 0) {
+        r = g.init ^ kConditioning;
+        for (uint32_t q = 0; q < g.h; ++q) r = feed_byte(r, readlane(ecur, q));
+        acc = 0;
+      }
+      // -- fold this chunk --
+      if (g.W) {
+        if (c == 0) {
+          const uint32_t jstart = g.pad >> 6;
+          const uint32_t l0 = g.pad & 63u;
+#pragma unroll
+          for (int j = 0; j < kRounds; ++j) {
+            if ((uint32_t)j < jstart) continue;
+            uint32_t w = cur[j];
+            if ((uint32_t)j == jstart) {
+              w = lane >= l0 ? w : 0u;
+              w ^= lane == l0 ? r : 0u;  // initial register enters with body word 0
+            }
+            acc = shift256(tab, acc) ^ w;
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < kRounds; ++j) acc = shift256(tab, acc) ^ cur[j];
+        }
+      }
+      // -- span end: per-lane realignment, wave reduction, tail, output --
+      if (c + 1 == g.nch) {
+        if (g.W) {
+          uint32_t v = 0;
+#pragma unroll
+          for (int i = 0; i < 32; ++i) v ^= M[i] & (0u - ((acc >> i) & 1u));
+          r = wave_xor(v);
+        }
+        for (uint32_t q = 0; q < g.t; ++q) r = feed_byte(r, readlane(ecur, 3u + q));
+        const uint32_t crc = r ^ kConditioning;
+        const uint64_t b = wave + k * nwaves;
+        if (lane == 0) {
+          if (a.out != nullptr) a.out[b] = (a.flags & kFlagMask) ? mask_crc(crc) : crc;
+          if (kVerify && a.mismatch != nullptr) {
+            const uint32_t stored = readlane(ecur, 6) | (readlane(ecur, 7) << 8) |
+                                    (readlane(ecur, 8) << 16) | (readlane(ecur, 9) << 24);
+            a.mismatch[b] = crc != unmask_crc(stored) ? 1 : 0;
+          }
+        }
+      }
+    }
+    if (!have_next) break;
+    k = k2;
+    c = c2;
+    g = g2;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Long-span planner: spans longer than kLongSpan become segments
+// [first piece of len - (nseg-1)*kSegment bytes with the span's init]
+// followed by nseg-1 pieces of kSegment bytes with init 0xFFFFFFFF (raw).
+// ---------------------------------------------------------------------------
+template <bool kDesc>
+__global__ __launch_bounds__(256) void crc32c_plan_kernel(SpanBatch a, SplitWs ws) {
+  const uint64_t n = a.n;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t len = kDesc ? a.len[i] : a.len_c;
+    if (len <= a.skip_above) continue;
+    const uint32_t nseg = (len + kSegment - 1u) / kSegment;
+    const uint32_t first = len - (nseg - 1u) * kSegment;
+    const uint64_t pos = atomicAdd((unsigned long long*)&ws.counters->nseg, (unsigned long long)nseg);
+    const uint32_t li = atomicAdd(&ws.counters->nlong, 1u);
+    if (pos + nseg > ws.cap_seg || li >= ws.cap_long) {
+      atomicOr(&ws.counters->overflow, 1u);
+      continue;
+    }
+    const uint64_t off = kDesc ? a.off[i] : i * a.stride;
+    const uint32_t init = kDesc ? (a.init != nullptr ? a.init[i] : 0u) : a.init_c;
+    ws.long_span[li] = i;
+    ws.long_first[li] = pos;
+    ws.long_nseg[li] = nseg;
+    ws.seg_off[pos] = off;
+    ws.seg_len[pos] = first;
+    ws.seg_init[pos] = init;
+    for (uint32_t s = 1; s < nseg; ++s) {
+      ws.seg_off[pos + s] = off + first + (uint64_t)(s - 1u) * kSegment;
+      ws.seg_len[pos + s] = kSegment;
+      ws.seg_init[pos + s] = kConditioning;  // Extend(0xFFFFFFFF, d) ^ ~0 == raw register R(0, d)
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Long-span combine: crc(A||B) with |B| = kSegment, one thread per long span.
+// ---------------------------------------------------------------------------
+template <bool kDesc, bool kVerify>
+__global__ __launch_bounds__(256) void crc32c_combine_kernel(SpanBatch a, SplitWs ws) {
+  if (ws.counters->overflow != 0u) return;
+  const uint32_t nlong = min(ws.counters->nlong, ws.cap_long);
+  for (uint32_t li = blockIdx.x * blockDim.x + threadIdx.x; li < nlong; li += gridDim.x * blockDim.x) {
+    const uint64_t span = ws.long_span[li];
+    const uint64_t first = ws.long_first[li];
+    const uint32_t nseg = ws.long_nseg[li];
+    uint32_t r = ws.seg_out[first] ^ kConditioning;
+    for (uint32_t s = 1; s < nseg; ++s) {
+      uint32_t y = 0;
+#pragma unroll
+      for (int i = 0; i < 32; ++i) y ^= a.tabs->shift_seg[i] & (0u - ((r >> i) & 1u));
+      r = y ^ ws.seg_out[first + s] ^ kConditioning;
+    }
+    const uint32_t crc = r ^ kConditioning;
+    if (a.out != nullptr) a.out[span] = (a.flags & kFlagMask) ? mask_crc(crc) : crc;
+    if (kVerify && a.mismatch != nullptr) {
+      const uint64_t off = kDesc ? a.off[span] : span * a.stride;
+      const uint32_t len = kDesc ? a.len[span] : a.len_c;
+      const uint8_t* t = a.base + off + len;
+      const uint32_t stored = (uint32_t)t[0] | ((uint32_t)t[1] << 8) | ((uint32_t)t[2] << 16) |
+                              ((uint32_t)t[3] << 24);
+      a.mismatch[span] = crc != unmask_crc(stored) ? 1 : 0;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Host-side launchers (called from crc32c_capi.cc through crc32c_device.h).
+// ---------------------------------------------------------------------------
+hipError_t launch_span(const SpanBatch& a, bool desc, bool verify, int grid, hipStream_t s) {
+  if (desc) {
+    if (verify) crc32c_span_kernel<true, true><<<grid, kThreads, 0, s>>>(a);
+    else crc32c_span_kernel<true, false><<<grid, kThreads, 0, s>>>(a);
+  } else {
+    if (verify) crc32c_span_kernel<false, true><<<grid, kThreads, 0, s>>>(a);
+    else crc32c_span_kernel<false, false><<<grid, kThreads, 0, s>>>(a);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_plan(const SpanBatch& a, bool desc, const SplitWs& ws, hipStream_t s) {
+  const uint64_t want = (a.n + 255u) / 256u;
+  const int grid = (int)(want < 4096u ? (want ? want : 1u) : 4096u);
+  if (desc) crc32c_plan_kernel<true><<<grid, 256, 0, s>>>(a, ws);
+  else crc32c_plan_kernel<false><<<grid, 256, 0, s>>>(a, ws);
+  return hipGetLastError();
+}
+
+hipError_t launch_combine(const SpanBatch& a, bool desc, bool verify, const SplitWs& ws,
+                          hipStream_t s) {
+  const int grid = 64;
+  if (desc) {
+    if (verify) crc32c_combine_kernel<true, true><<<grid, 256, 0, s>>>(a, ws);
+    else crc32c_combine_kernel<true, false><<<grid, 256, 0, s>>>(a, ws);
+  } else {
+    if (verify) crc32c_combine_kernel<false, true><<<grid, 256, 0, s>>>(a, ws);
+    else crc32c_combine_kernel<false, false><<<grid, 256, 0, s>>>(a, ws);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace dev
+}  // namespace prismdb
