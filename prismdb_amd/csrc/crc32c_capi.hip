@@ -79,17 +79,24 @@ int SelfTest(DeviceCtx& ctx) {
                             leveldb_crc32c_value(reinterpret_cast<const char*>(h) + 64, 4096),
                             leveldb_crc32c_value(reinterpret_cast<const char*>(h) + 64 + 4096, kBig)};
   unsigned char* d = nullptr;
-  hipError_t e = hipMalloc(&d, bytes + 3 * 8 + 3 * 4 + 3 * 4);
+  const size_t desc_at = (bytes + 15) & ~size_t(15);
+  hipError_t e = hipMalloc(&d, desc_at + 64);
   if (e != hipSuccess) {
     delete[] h;
     return FailHip(e, "self-test hipMalloc");
   }
-  uint64_t* d_off = reinterpret_cast<uint64_t*>(d + ((bytes + 7) & ~size_t(7)));
-  uint32_t* d_len = reinterpret_cast<uint32_t*>(d_off + 3);
-  uint32_t* d_out = d_len + 3;
-  hipMemcpy(d, h, bytes, hipMemcpyHostToDevice);
-  hipMemcpy(d_off, off, sizeof(off), hipMemcpyHostToDevice);
-  hipMemcpy(d_len, len, sizeof(len), hipMemcpyHostToDevice);
+  uint64_t* d_off = reinterpret_cast<uint64_t*>(d + desc_at);  // 24 B
+  uint32_t* d_len = reinterpret_cast<uint32_t*>(d_off + 3);     // 12 B
+  uint32_t* d_out = d_len + 3;                                  // 12 B
+  e = hipMemcpy(d, h, bytes, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(d_off, off, sizeof(off), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(d_len, len, sizeof(len), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemset(d_out, 0, sizeof(uint32_t) * 3);
+  if (e != hipSuccess) {
+    hipFree(d);
+    delete[] h;
+    return FailHip(e, "self-test upload");
+  }
   SpanBatch a{};
   a.base = d;
   a.off = d_off;
@@ -102,16 +109,18 @@ int SelfTest(DeviceCtx& ctx) {
     e = hipStreamSynchronize(nullptr);
     if (e != hipSuccess) rc = FailHip(e, "self-test sync");
   }
-  if (rc == 0) hipMemcpy(got, d_out, sizeof(got), hipMemcpyDeviceToHost);
+  if (rc == 0) {
+    e = hipMemcpy(got, d_out, sizeof(got), hipMemcpyDeviceToHost);
+    if (e != hipSuccess) rc = FailHip(e, "self-test download");
+  }
   hipFree(d);
   delete[] h;
   if (rc != 0) return rc;
-  for (int i = 0; i < 3; ++i) {
-    if (got[i] != want[i]) {
-      char buf[160];
-      std::snprintf(buf, sizeof(buf), "device self-test %d: got %08x want %08x", i, got[i], want[i]);
-      return Fail(PRISMDB_CRC32C_ESELFTEST, buf);
-    }
+  if (got[0] != want[0] || got[1] != want[1] || got[2] != want[2]) {
+    char buf[200];
+    std::snprintf(buf, sizeof(buf), "device self-test: got %08x %08x %08x want %08x %08x %08x", got[0],
+                  got[1], got[2], want[0], want[1], want[2]);
+    return Fail(PRISMDB_CRC32C_ESELFTEST, buf);
   }
   return 0;
 }

@@ -1,0 +1,11 @@
+#!/bin/bash
+# Round-1 GPU call: parity tests, smoke, short bench.  A test/assert failure
+# (rc 1) does not stop the later steps; a crash, abort or timeout does.
+cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out
+ok() { [ "$1" -eq 0 ] || [ "$1" -eq 1 ]; }
+timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider > gpurun_out/gpu_tests.log 2>&1
+rc=$?; echo "pytest rc=$rc" >> gpurun_out/gpu_tests.log; ok $rc || exit $rc
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
+rc=$?; echo "smoke rc=$rc" >> gpurun_out/smoke.log; ok $rc || exit $rc
+timeout -k 10 600 python bench.py --steps 10 --warmup 2 > gpurun_out/bench.log 2>&1
