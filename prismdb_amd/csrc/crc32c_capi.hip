@@ -47,12 +47,16 @@ struct DeviceCtx {
 
 DeviceCtx g_ctx[kMaxDevices];
 
+// Test hook: route fixed-stride batches through the generic span kernel.
+bool g_force_generic = false;
+
 void BuildTables(DeviceTables* t) {
   namespace g = prismdb::gf2;
   g::StrideTables(prismdb::dev::kStrideBytes, t->stride);
   for (int l = 0; l < 64; ++l) {
     const g::Op m = g::ShiftBytes(prismdb::dev::kStrideBytes - 4u * (uint32_t)l);
-    for (int i = 0; i < 32; ++i) t->lane_mat[l][i] = m.col[i];
+    for (int n = 0; n < 8; ++n)
+      for (uint32_t v = 0; v < 16; ++v) t->lane_nib[n][v][l] = g::Apply(m, v << (4 * n));
   }
   const g::Op s = g::ShiftBytes(prismdb::dev::kSegment);
   for (int i = 0; i < 32; ++i) t->shift_seg[i] = s.col[i];
@@ -209,6 +213,13 @@ int RunBatch(DeviceCtx& ctx, const SpanBatch& base_args, bool desc, bool verify,
   a.tabs = ctx.tabs;
   a.role = prismdb::dev::kRoleSpans;
   const bool may_be_long = desc || a.len_c > prismdb::dev::kLongSpan;
+  // Fast path: fixed stride, 4-byte aligned, 4..4096-byte multiple-of-4 spans.
+  if (!desc && !verify && a.out != nullptr && a.len_c >= 4 && a.len_c <= 4u * prismdb::dev::kChunkWords &&
+      (a.len_c & 3u) == 0 && (a.stride & 3u) == 0 && (reinterpret_cast<uintptr_t>(a.base) & 3u) == 0 &&
+      !g_force_generic) {
+    hipError_t e = prismdb::dev::launch_fixed(a, ctx.cus, s);
+    return e == hipSuccess ? 0 : FailHip(e, "fixed kernel launch");
+  }
   if (!may_be_long) {
     a.skip_above = 0xFFFFFFFFu;
     a.overflow = nullptr;
@@ -307,5 +318,8 @@ int leveldb_crc32c_batch(const void* dev_base, const uint64_t* dev_off, const ui
 }
 
 const char* leveldb_crc32c_last_error(void) { return t_last_error.c_str(); }
+
+// Not in the public header: lets the parity tests pin the generic kernel too.
+void prismdb_crc32c_force_generic(int on) { g_force_generic = on != 0; }
 
 }  // extern "C"

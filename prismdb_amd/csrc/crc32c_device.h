@@ -19,7 +19,9 @@ constexpr int kRounds = 16;                        // 256-B rounds per chunk
 constexpr uint32_t kChunkWords = kRounds * kWave;  // 1024 words = 4 KiB per chunk
 constexpr uint32_t kStrideBytes = 4u * kWave;      // 256 B between a lane's words
 constexpr int kCopies = 32;                        // LDS table replication (bank = lane % 32)
-constexpr int kTabWords = 4 * 256 * kCopies;       // 128 KiB of LDS
+constexpr int kTabWords = 4 * 256 * kCopies;       // 128 KiB of LDS: stride tables
+constexpr int kNibWords = 8 * 16 * kWave;          // 32 KiB of LDS: per-lane realignment tables
+constexpr int kLdsWords = kTabWords + kNibWords;   // 160 KiB: all of a CU's LDS
 
 constexpr uint32_t kLongSpan = 128u * 1024u;       // spans above this are split...
 constexpr uint32_t kSegment = 32u * 1024u;         // ...into pieces of this size
@@ -27,7 +29,7 @@ constexpr uint32_t kSegment = 32u * 1024u;         // ...into pieces of this siz
 // Tables derived on the host from the polynomial (crc32c_gf2.h) and kept in HBM.
 struct DeviceTables {
   uint32_t stride[4][256];    // stride[k][b] = shift_256(b << 8k)
-  uint32_t lane_mat[64][32];  // column i of shift_{256-4l} for lane l
+  uint32_t lane_nib[8][16][64];  // [n][v][l] = shift_{256-4l}(v << 4n): lane l's realignment
   uint32_t shift_seg[32];     // column i of shift_kSegment
 };
 
@@ -72,6 +74,7 @@ struct SplitWs {
 };
 
 hipError_t launch_span(const SpanBatch& a, bool desc, bool verify, int grid, hipStream_t s);
+hipError_t launch_fixed(const SpanBatch& a, int grid, hipStream_t s);
 hipError_t launch_plan(const SpanBatch& a, bool desc, const SplitWs& ws, hipStream_t s);
 hipError_t launch_combine(const SpanBatch& a, bool desc, bool verify, const SplitWs& ws,
                           hipStream_t s);

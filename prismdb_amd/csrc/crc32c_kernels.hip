@@ -31,6 +31,10 @@
 
 #include "crc32c_device.h"
 
+#ifndef PRISMDB_NT_LOADS
+#define PRISMDB_NT_LOADS 1  // body words are read once: non-temporal
+#endif
+
 namespace prismdb {
 namespace dev {
 
@@ -101,33 +105,54 @@ __device__ __forceinline__ uint32_t shift256(const uint32_t* __restrict__ tab, u
   return a0 ^ a1 ^ a2 ^ a3;
 }
 
+__device__ __forceinline__ uint32_t load_word(const uint8_t* p) {
+#if PRISMDB_NT_LOADS
+  return __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(p));
+#else
+  return *reinterpret_cast<const uint32_t*>(p);
+#endif
+}
+
+// shift_{256-4l}(acc) for this lane: eight nibble lookups in lane l's own
+// tables (entry [n][v] at word 64*(16n+v)+l, so bank = l mod 32).
+__device__ __forceinline__ uint32_t realign(const uint32_t* __restrict__ nibtab, uint32_t acc) {
+  uint32_t v = 0;
+#pragma unroll
+  for (int n = 0; n < 8; ++n) v ^= nibtab[(uint32_t)(16 * n) * 64u + (((acc >> (4 * n)) & 15u) << 6)];
+  return v;
+}
+
 // Issue the body loads of chunk c of g into w[] (no wait).
 __device__ __forceinline__ void issue_chunk(const Geo& g, uint32_t c, uint32_t lane,
                                             uint32_t (&w)[kRounds]) {
-  const uint32_t* body = reinterpret_cast<const uint32_t*>(g.p + g.h);
+  const uint8_t* body = g.p + g.h;
   const int32_t i0 = (int32_t)(c * kChunkWords + lane) - (int32_t)g.pad;
   if (c == 0 && g.pad != 0) {
 #pragma unroll
     for (int j = 0; j < kRounds; ++j) {
       const int32_t i = i0 + 64 * j;
-      w[j] = __builtin_nontemporal_load(body + (i < 0 ? 0 : i));
+      const uint32_t byte_off = (uint32_t)(i < 0 ? 0 : i) * 4u;
+      w[j] = load_word(body + byte_off);
     }
   } else {
+    const uint32_t byte_off = (uint32_t)i0 * 4u;
 #pragma unroll
-    for (int j = 0; j < kRounds; ++j) w[j] = __builtin_nontemporal_load(body + i0 + 64 * j);
+    for (int j = 0; j < kRounds; ++j) w[j] = load_word(body + byte_off + 256u * j);
   }
 }
 
-// Issue the edge-byte load of a span: lanes 0..h-1 head, 3..3+t-1 tail,
-// 6..9 stored trailer (verify).
+// Issue the edge-byte load of chunk c of a span into the chunk's own slot:
+// lanes 0..h-1 head bytes (first chunk), 3..3+t-1 tail bytes and 6..9 the
+// stored trailer (verify) (last chunk).
 template <bool kVerify>
-__device__ __forceinline__ uint32_t issue_edges(const Geo& g, uint32_t lane) {
+__device__ __forceinline__ uint32_t issue_edges(const Geo& g, uint32_t c, uint32_t lane) {
   const uint8_t* src = nullptr;
-  if (lane < g.h)
+  const bool first = c == 0, last = c + 1 == g.nch;
+  if (first && lane < g.h)
     src = g.p + lane;
-  else if (lane >= 3u && lane < 3u + g.t)
+  else if (last && lane >= 3u && lane < 3u + g.t)
     src = g.p + g.h + 4ull * g.W + (lane - 3u);
-  else if (kVerify && lane >= 6u && lane < 10u)
+  else if (kVerify && last && lane >= 6u && lane < 10u)
     src = g.p + g.len + (lane - 6u);
   uint32_t e = 0;
   if (src != nullptr) e = *src;
@@ -157,19 +182,19 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
   }
   if (n == 0) return;
 
-  __shared__ uint32_t lds[kTabWords];
+  __shared__ uint32_t lds[kLdsWords];
   const uint32_t tid = threadIdx.x;
   {
     const uint32_t* src = &a.tabs->stride[0][0];
     for (uint32_t e = tid; e < (uint32_t)kTabWords; e += kThreads) lds[e] = src[e >> 5];
+    const uint32_t* nib = &a.tabs->lane_nib[0][0][0];
+    for (uint32_t e = tid; e < (uint32_t)kNibWords; e += kThreads) lds[kTabWords + e] = nib[e];
   }
   const uint32_t lane = tid & 63u;
-  uint32_t M[32];
-#pragma unroll
-  for (int i = 0; i < 32; ++i) M[i] = a.tabs->lane_mat[lane][i];
   __syncthreads();
 
   const uint32_t* tab = lds + (lane & 31u);
+  const uint32_t* nibtab = lds + kTabWords + lane;
   const uint64_t wave = rfl(blockIdx.x * kWavesPerGroup + (tid >> 6));
   const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerGroup;
   if (wave >= n) return;
@@ -209,46 +234,67 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
     dnx = load_desc(1);
   }
 
-  uint64_t k = 0;  // span ordinal within this wave
-  uint32_t c = 0;  // chunk within the span
-  Geo g = geo_of(0);
-  uint32_t nx[kRounds];
-  uint32_t enx = 0;
-  if (!g.skip) {
-    if (g.W) issue_chunk(g, 0, lane, nx);
-    if (g.h | g.t | (uint32_t)kVerify) enx = issue_edges<kVerify>(g, lane);
-  }
-
-  uint32_t r = 0, acc = 0, ecur = 0;
-  while (true) {
-    uint32_t cur[kRounds];
-#pragma unroll
-    for (int j = 0; j < kRounds; ++j) cur[j] = nx[j];
-    if (c == 0) ecur = enx;
-
-    // -- next task and its loads (issued before this chunk is folded) --
-    uint64_t k2 = k;
-    uint32_t c2 = c + 1;
-    if (c2 == g.nch) {
-      k2 = k + 1;
-      c2 = 0;
-    }
-    const bool have_next = wave + k2 * nwaves < n;
-    Geo g2 = g;
-    if (have_next) {
-      if (c2 == 0) {
-        if (kDesc && (k2 & 63u) == 0) {
+  // --- task ring: task = (span ordinal k, chunk c); loads run kPrefetch tasks ahead ---
+  struct Task {
+    uint64_t k;
+    uint32_t c;
+    bool valid;
+    Geo g;
+  };
+  auto first_task = [&]() -> Task {
+    Task t;
+    t.k = 0;
+    t.c = 0;
+    t.valid = true;
+    t.g = geo_of(0);
+    return t;
+  };
+  auto next_task = [&](const Task& t) -> Task {
+    Task u = t;
+    u.c = t.c + 1;
+    if (u.c == t.g.nch) {
+      u.k = t.k + 1;
+      u.c = 0;
+      u.valid = t.valid && wave + u.k * nwaves < n;
+      if (u.valid) {
+        if (kDesc && (u.k & 63u) == 0) {
           dcur = dnx;
-          dnx = load_desc((k2 >> 6) + 1);
+          dnx = load_desc((u.k >> 6) + 1);
         }
-        g2 = geo_of(k2);
-      }
-      if (!g2.skip) {
-        if (g2.W) issue_chunk(g2, c2, lane, nx);
-        if (c2 == 0 && (g2.h | g2.t | (uint32_t)kVerify)) enx = issue_edges<kVerify>(g2, lane);
+        u.g = geo_of(u.k);
       }
     }
+    return u;
+  };
+  auto issue = [&](const Task& t, uint32_t (&w)[kRounds], uint32_t& e) {
+    if (t.valid && !t.g.skip) {
+      if (t.g.W) issue_chunk(t.g, t.c, lane, w);
+      if ((t.c == 0 && t.g.h) || (t.c + 1 == t.g.nch && (t.g.t | (uint32_t)kVerify)))
+        e = issue_edges<kVerify>(t.g, t.c, lane);
+    }
+  };
 
+  // Three chunk buffers in a ring, the loop unrolled three times so every
+  // buffer keeps a static register name (a register copy between ring slots
+  // would force a vmcnt(0) on the freshest loads and undo the prefetch).
+  Task t0 = first_task();
+  Task t1 = next_task(t0);
+  uint32_t bA[kRounds], bB[kRounds], bC[kRounds];
+#pragma unroll
+  for (int j = 0; j < kRounds; ++j) bA[j] = bB[j] = bC[j] = 0u;
+  uint32_t eA = 0, eB = 0, eC = 0;
+  issue(t0, bA, eA);
+  issue(t1, bB, eB);
+
+  uint32_t r = 0, acc = 0;
+  // Fold t0 (data in `cur`, edge bytes in `ecur`), first issuing t0+2 into `nxt`.
+  auto step = [&](uint32_t (&cur)[kRounds], uint32_t ecur, uint32_t (&nxt)[kRounds],
+                  uint32_t& enxt) -> bool {
+    const Task t2 = next_task(t1);
+    issue(t2, nxt, enxt);  // two tasks ahead of the one folded below
+
+    const Geo& g = t0.g;
+    const uint32_t c = t0.c;
     if (!g.skip) {
       // -- span start: initial register through the head bytes --
       if (c == 0) {
@@ -279,14 +325,11 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
       // -- span end: per-lane realignment, wave reduction, tail, output --
       if (c + 1 == g.nch) {
         if (g.W) {
-          uint32_t v = 0;
-#pragma unroll
-          for (int i = 0; i < 32; ++i) v ^= M[i] & (0u - ((acc >> i) & 1u));
-          r = wave_xor(v);
+          r = wave_xor(realign(nibtab, acc));
         }
         for (uint32_t q = 0; q < g.t; ++q) r = feed_byte(r, readlane(ecur, 3u + q));
         const uint32_t crc = r ^ kConditioning;
-        const uint64_t b = wave + k * nwaves;
+        const uint64_t b = wave + t0.k * nwaves;
         if (lane == 0) {
           if (a.out != nullptr) a.out[b] = (a.flags & kFlagMask) ? mask_crc(crc) : crc;
           if (kVerify && a.mismatch != nullptr) {
@@ -297,11 +340,132 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
         }
       }
     }
-    if (!have_next) break;
-    k = k2;
-    c = c2;
-    g = g2;
+    if (!t1.valid) return false;
+    t0 = t1;
+    t1 = t2;
+    return true;
+  };
+  while (step(bA, eA, bC, eC) && step(bB, eB, bA, eA) && step(bC, eC, bB, eB)) {
   }
+}
+
+// Inline-asm dword load, non-temporal, SGPR base + 32-bit VGPR byte offset.
+// The compiler does not track these: consumers must go through wait_ring.
+template <int kImm>
+__device__ __forceinline__ uint32_t asm_load_dword(const uint8_t* base, uint32_t voff) {
+  uint32_t r;
+  asm volatile("global_load_dword %0, %1, %2 offset:%3 nt" : "=v"(r) : "v"(voff), "s"(base), "n"(kImm));
+  return r;
+}
+
+// Round j (1..K-1) of a span: immediate offset 256*(j-1) from off1.
+template <int K>
+__device__ __forceinline__ uint32_t asm_load_dword_at(const uint8_t* base, uint32_t off1, int j) {
+  switch (j) {
+    case 1: return asm_load_dword<0>(base, off1);
+    case 2: return asm_load_dword<256>(base, off1);
+    case 3: return asm_load_dword<512>(base, off1);
+    case 4: return asm_load_dword<768>(base, off1);
+    case 5: return asm_load_dword<1024>(base, off1);
+    case 6: return asm_load_dword<1280>(base, off1);
+    case 7: return asm_load_dword<1536>(base, off1);
+    case 8: return asm_load_dword<1792>(base, off1);
+    case 9: return asm_load_dword<2048>(base, off1);
+    case 10: return asm_load_dword<2304>(base, off1);
+    case 11: return asm_load_dword<2560>(base, off1);
+    case 12: return asm_load_dword<2816>(base, off1);
+    case 13: return asm_load_dword<3072>(base, off1);
+    case 14: return asm_load_dword<3328>(base, off1);
+    default: return asm_load_dword<3584>(base, off1);
+  }
+}
+
+// Wait until this buffer's K loads have landed while the two buffers issued
+// after it (2K loads) stay in flight; output stores issued in between only
+// make the wait stricter, never short.  The buffer registers are in/out
+// operands so no consumer can be scheduled above the wait.
+template <int K>
+__device__ __forceinline__ void wait_ring(uint32_t (&w)[kRounds]) {
+  asm volatile("s_waitcnt vmcnt(%16)"
+               : "+v"(w[0]), "+v"(w[1]), "+v"(w[2]), "+v"(w[3]), "+v"(w[4]), "+v"(w[5]), "+v"(w[6]),
+                 "+v"(w[7]), "+v"(w[8]), "+v"(w[9]), "+v"(w[10]), "+v"(w[11]), "+v"(w[12]),
+                 "+v"(w[13]), "+v"(w[14]), "+v"(w[15])
+               : "n"(2 * K)
+               : "memory");
+}
+
+// ---------------------------------------------------------------------------
+// Fixed-geometry fast path: every span is len bytes at base + i*stride with
+// base, stride and len multiples of 4 and len <= 4 KiB, so a span is K rounds
+// (K = ceil(len/256), a template parameter) with no head/tail bytes and the
+// same padding (pk = 64K - len/4 leading zero words, all in round 0).
+// Straight-line ring of three span buffers (loop unrolled x3): the loads of
+// span k+2 are in flight while span k is folded; counted vmcnt waits only.
+// ---------------------------------------------------------------------------
+template <int K>
+__global__ __launch_bounds__(kThreads) void crc32c_fixed_kernel(SpanBatch a) {
+  const uint64_t n = a.n;
+  __shared__ uint32_t lds[kLdsWords];
+  const uint32_t tid = threadIdx.x;
+  {
+    const uint32_t* src = &a.tabs->stride[0][0];
+    for (uint32_t e = tid; e < (uint32_t)kTabWords; e += kThreads) lds[e] = src[e >> 5];
+    const uint32_t* nib = &a.tabs->lane_nib[0][0][0];
+    for (uint32_t e = tid; e < (uint32_t)kNibWords; e += kThreads) lds[kTabWords + e] = nib[e];
+  }
+  const uint32_t lane = tid & 63u;
+  __syncthreads();
+  const uint32_t* tab = lds + (lane & 31u);
+  const uint32_t* nibtab = lds + kTabWords + lane;
+  const uint64_t wave = rfl(blockIdx.x * kWavesPerGroup + (tid >> 6));
+  const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerGroup;
+  if (wave >= n) return;
+
+  const uint32_t pk = 64u * K - (a.len_c >> 2);  // 0..63 leading zero words (round 0)
+  const uint32_t r0 = a.init_c ^ kConditioning;
+  const bool masked = (a.flags & kFlagMask) != 0;
+  const int32_t w0 = (int32_t)lane - (int32_t)pk;   // word index of round 0
+  const uint32_t off0 = (uint32_t)(w0 < 0 ? 0 : w0) * 4u;
+  const uint32_t off1 = (uint32_t)(w0 + 64) * 4u;   // rounds >= 1 never clamp
+
+  // The ring's loads are issued with inline asm and retired with explicit
+  // counted waits (hipcc's own waitcnt pass merges the ring's scoreboards into
+  // vmcnt(0), which would drain the prefetch).  Unconditional: a span past the
+  // end re-reads the last one.  Every buffer is exactly K loads.
+  auto issue = [&](uint64_t k, uint32_t (&w)[kRounds]) {
+    uint64_t b = wave + k * nwaves;
+    b = b < n ? b : n - 1;
+    const uint8_t* p = a.base + b * a.stride;
+    w[0] = asm_load_dword<0>(p, off0);
+#pragma unroll
+    for (int j = 1; j < K; ++j) w[j] = asm_load_dword_at<K>(p, off1, j);
+  };
+  auto fold = [&](uint64_t k, uint32_t (&w)[kRounds]) {
+    wait_ring<K>(w);  // the two younger buffers (2K loads) may stay in flight
+    uint32_t x = lane >= pk ? w[0] : 0u;
+    x ^= lane == pk ? r0 : 0u;  // initial register enters with body word 0
+    uint32_t acc = x;
+#pragma unroll
+    for (int j = 1; j < K; ++j) acc = shift256(tab, acc) ^ w[j];
+    const uint32_t crc = wave_xor(realign(nibtab, acc)) ^ kConditioning;
+    if (lane == 0) a.out[wave + k * nwaves] = masked ? mask_crc(crc) : crc;
+  };
+
+  uint32_t bA[kRounds], bB[kRounds], bC[kRounds];
+  issue(0, bA);
+  issue(1, bB);
+  for (uint64_t k = 0;; k += 3) {
+    issue(k + 2, bC);
+    fold(k, bA);
+    if (wave + (k + 1) * nwaves >= n) break;
+    issue(k + 3, bA);
+    fold(k + 1, bB);
+    if (wave + (k + 2) * nwaves >= n) break;
+    issue(k + 4, bB);
+    fold(k + 2, bC);
+    if (wave + (k + 3) * nwaves >= n) break;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the ring's extra prefetches
 }
 
 // ---------------------------------------------------------------------------
@@ -381,6 +545,24 @@ hipError_t launch_span(const SpanBatch& a, bool desc, bool verify, int grid, hip
   } else {
     if (verify) crc32c_span_kernel<false, true><<<grid, kThreads, 0, s>>>(a);
     else crc32c_span_kernel<false, false><<<grid, kThreads, 0, s>>>(a);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_fixed(const SpanBatch& a, int grid, hipStream_t s) {
+  const int rounds = (int)((a.len_c + 255u) / 256u);  // 1..16
+  switch (rounds) {
+#define PRISMDB_CASE(K) \
+  case K:               \
+    crc32c_fixed_kernel<K><<<grid, kThreads, 0, s>>>(a); \
+    break;
+    PRISMDB_CASE(1) PRISMDB_CASE(2) PRISMDB_CASE(3) PRISMDB_CASE(4)
+    PRISMDB_CASE(5) PRISMDB_CASE(6) PRISMDB_CASE(7) PRISMDB_CASE(8)
+    PRISMDB_CASE(9) PRISMDB_CASE(10) PRISMDB_CASE(11) PRISMDB_CASE(12)
+    PRISMDB_CASE(13) PRISMDB_CASE(14) PRISMDB_CASE(15) PRISMDB_CASE(16)
+#undef PRISMDB_CASE
+    default:
+      return hipErrorInvalidValue;
   }
   return hipGetLastError();
 }

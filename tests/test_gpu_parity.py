@@ -77,7 +77,19 @@ def test_long_stream_vectors_device(dev, golden):
         assert crc32c.as_u32(out) == [s["crc"]], s
 
 
-def test_fixed_4k_blocks_vs_oracle(dev, oracle):
+@pytest.fixture(params=["fast", "generic"])
+def kernel_path(request, native):
+    """Run fixed-stride cases through the fixed-geometry kernel and, forced,
+    through the generic span kernel."""
+    import ctypes
+
+    native.prismdb_crc32c_force_generic.argtypes = [ctypes.c_int]
+    native.prismdb_crc32c_force_generic(1 if request.param == "generic" else 0)
+    yield request.param
+    native.prismdb_crc32c_force_generic(0)
+
+
+def test_fixed_4k_blocks_vs_oracle(dev, oracle, kernel_path):
     """Config-2 shape (4 KiB blocks, stride 4096) at 64 Ki blocks, all checked."""
     import torch
     from prismdb_amd import crc32c
@@ -96,8 +108,9 @@ def test_fixed_4k_blocks_vs_oracle(dev, oracle):
 
 
 @pytest.mark.parametrize("stride,length", [(4096, 4095), (3992, 3988), (3993, 3988), (64, 61), (8192, 7),
-                                           (1, 1), (4096, 0), (300000, 262147)])
-def test_fixed_odd_geometries(dev, oracle, stride, length):
+                                           (1, 1), (4096, 0), (300000, 262147), (4096, 4), (4096, 256),
+                                           (4100, 260), (2048, 2044), (8, 8), (4, 4), (12, 8), (5000, 4092)])
+def test_fixed_odd_geometries(dev, oracle, stride, length, kernel_path):
     import torch
     from prismdb_amd import crc32c
 
