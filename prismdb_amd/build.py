@@ -50,9 +50,15 @@ def _run(cmd: list[str]) -> None:
         raise RuntimeError("build failed:\n" + " ".join(cmd) + "\n" + r.stdout)
 
 
-def build(force: bool = False, asm: bool = False, verbose: bool = False) -> str:
-    os.makedirs(LIBDIR, exist_ok=True)
-    os.makedirs(OBJDIR, exist_ok=True)
+def build(force: bool = False, asm: bool = False, verbose: bool = False, defines: dict | None = None,
+          lib_path: str | None = None) -> str:
+    """Build the library.  `defines`/`lib_path` build a tuning variant
+    (e.g. {"PRISMDB_RING": 3}) to a separate file; the product is the default."""
+    lib_out = lib_path or LIB
+    objdir = OBJDIR if not defines else os.path.join(ROOT, "build", "obj_" + "_".join(
+        f"{k}{v}" for k, v in sorted(defines.items())))
+    os.makedirs(os.path.dirname(lib_out), exist_ok=True)
+    os.makedirs(objdir, exist_ok=True)
     hipcc = _hipcc()
     headers = [os.path.join(CSRC, h) for h in HEADERS] + [
         os.path.join(ROOT, "include", "prismdb_crc32c.h"),
@@ -60,11 +66,12 @@ def build(force: bool = False, asm: bool = False, verbose: bool = False) -> str:
         os.path.join(ROOT, "include", "util", "crc32c.h"),
     ]
     common = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function"]
+    common += [f"-D{k}={v}" for k, v in sorted((defines or {}).items())]
     jobs = []
     objs = []
     for src in HIP_SOURCES + CXX_SOURCES:
         s = os.path.join(CSRC, src)
-        o = os.path.join(OBJDIR, src + ".o")
+        o = os.path.join(objdir, src + ".o")
         objs.append(o)
         if force or _stale(o, [s] + headers):
             if src.endswith(".hip"):
@@ -77,15 +84,15 @@ def build(force: bool = False, asm: bool = False, verbose: bool = False) -> str:
             if verbose:
                 print(" ".join(cmd))
         list(ex.map(_run, jobs))
-    if force or jobs or _stale(LIB, objs):
-        _run([hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", LIB, *objs])
+    if force or jobs or _stale(lib_out, objs):
+        _run([hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", lib_out, *objs])
     if asm:
         asmdir = os.path.join(ROOT, "build", "asm")
         os.makedirs(asmdir, exist_ok=True)
         for src in HIP_SOURCES:
             _run([hipcc, "-x", "hip", f"--offload-arch={ARCH}", *common, "--cuda-device-only", "-S",
                   os.path.join(CSRC, src), "-o", os.path.join(asmdir, src + ".s")])
-    return LIB
+    return lib_out
 
 
 def main() -> int:

@@ -31,6 +31,9 @@
 
 #include "crc32c_device.h"
 
+#ifndef PRISMDB_RING
+#define PRISMDB_RING 4  // span buffers in the fixed kernel's prefetch ring (even)
+#endif
 #ifndef PRISMDB_NT_LOADS
 #define PRISMDB_NT_LOADS 1  // body words are read once: non-temporal
 #endif
@@ -96,13 +99,45 @@ __device__ __forceinline__ Geo make_geo(const uint8_t* p, uint32_t len, uint32_t
   return g;
 }
 
-// shift_256(acc): four LDS lookups, lane-private bank (see header comment).
-__device__ __forceinline__ uint32_t shift256(const uint32_t* __restrict__ tab, uint32_t acc) {
-  const uint32_t a0 = tab[(acc & 0xffu) << 5];
-  const uint32_t a1 = tab[(1u << 13) + (((acc >> 8) & 0xffu) << 5)];
-  const uint32_t a2 = tab[(2u << 13) + (((acc >> 16) & 0xffu) << 5)];
-  const uint32_t a3 = tab[(3u << 13) + ((acc >> 24) << 5)];
-  return a0 ^ a1 ^ a2 ^ a3;
+// LDS image of the stride tables (128 KiB): table k, entry e, copy c = lane%32
+// sits at byte ((k>>1) << 16) | (e << 8) | ((k&1) << 7) | (c << 2), so every
+// lookup address is one v_perm_b32: byte 1 <- byte k of acc, bytes 0 and 2
+// from a per-lane constant.  Bank = c: ds_read_b32 never conflicts.
+struct StrideLanes {
+  uint32_t L[4];  // per-lane byte-0/byte-2 constants of tables 0..3
+};
+
+__device__ __forceinline__ StrideLanes stride_lanes(uint32_t lane) {
+  StrideLanes t;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) t.L[k] = ((uint32_t)(k & 1) << 7) | ((lane & 31u) << 2) | ((uint32_t)(k >> 1) << 16);
+  return t;
+}
+
+// Fill LDS: stride tables in the image above, then the per-lane nibble tables.
+__device__ __forceinline__ void load_tables(uint32_t* lds, const DeviceTables* tabs, uint32_t tid) {
+  for (uint32_t w = tid; w < (uint32_t)kTabWords; w += kThreads) {
+    const uint32_t k = ((w >> 14) << 1) | ((w >> 5) & 1u), e = (w >> 6) & 255u;
+    lds[w] = tabs->stride[k][e];
+  }
+  const uint32_t* nib = &tabs->lane_nib[0][0][0];
+  for (uint32_t e = tid; e < (uint32_t)kNibWords; e += kThreads) lds[kTabWords + e] = nib[e];
+}
+
+__device__ __forceinline__ uint32_t lds_word(const uint32_t* lds, uint32_t byte_addr) {
+  return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(lds) + byte_addr);
+}
+
+// One stream step: shift_256(acc) ^ w with four conflict-free LDS lookups
+// (w is folded in early so only one XOR trails the last lookup).
+__device__ __forceinline__ uint32_t step256(const uint32_t* lds, const StrideLanes& t, uint32_t acc,
+                                            uint32_t w) {
+  const uint32_t a0 = lds_word(lds, __builtin_amdgcn_perm(acc, t.L[0], 0x0C020400u));
+  const uint32_t a1 = lds_word(lds, __builtin_amdgcn_perm(acc, t.L[1], 0x0C020500u));
+  const uint32_t a2 = lds_word(lds, __builtin_amdgcn_perm(acc, t.L[2], 0x0C020600u));
+  const uint32_t a3 = lds_word(lds, __builtin_amdgcn_perm(acc, t.L[3], 0x0C020700u));
+  const uint32_t x = w ^ a0 ^ a1;
+  return x ^ a2 ^ a3;
 }
 
 __device__ __forceinline__ uint32_t load_word(const uint8_t* p) {
@@ -184,16 +219,11 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
 
   __shared__ uint32_t lds[kLdsWords];
   const uint32_t tid = threadIdx.x;
-  {
-    const uint32_t* src = &a.tabs->stride[0][0];
-    for (uint32_t e = tid; e < (uint32_t)kTabWords; e += kThreads) lds[e] = src[e >> 5];
-    const uint32_t* nib = &a.tabs->lane_nib[0][0][0];
-    for (uint32_t e = tid; e < (uint32_t)kNibWords; e += kThreads) lds[kTabWords + e] = nib[e];
-  }
+  load_tables(lds, a.tabs, tid);
   const uint32_t lane = tid & 63u;
   __syncthreads();
 
-  const uint32_t* tab = lds + (lane & 31u);
+  const StrideLanes tab = stride_lanes(lane);
   const uint32_t* nibtab = lds + kTabWords + lane;
   const uint64_t wave = rfl(blockIdx.x * kWavesPerGroup + (tid >> 6));
   const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerGroup;
@@ -315,11 +345,11 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
               w = lane >= l0 ? w : 0u;
               w ^= lane == l0 ? r : 0u;  // initial register enters with body word 0
             }
-            acc = shift256(tab, acc) ^ w;
+            acc = step256(lds, tab, acc, w);
           }
         } else {
 #pragma unroll
-          for (int j = 0; j < kRounds; ++j) acc = shift256(tab, acc) ^ cur[j];
+          for (int j = 0; j < kRounds; ++j) acc = step256(lds, tab, acc, cur[j]);
         }
       }
       // -- span end: per-lane realignment, wave reduction, tail, output --
@@ -354,7 +384,11 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
 template <int kImm>
 __device__ __forceinline__ uint32_t asm_load_dword(const uint8_t* base, uint32_t voff) {
   uint32_t r;
+#if PRISMDB_NT_LOADS
   asm volatile("global_load_dword %0, %1, %2 offset:%3 nt" : "=v"(r) : "v"(voff), "s"(base), "n"(kImm));
+#else
+  asm volatile("global_load_dword %0, %1, %2 offset:%3" : "=v"(r) : "v"(voff), "s"(base), "n"(kImm));
+#endif
   return r;
 }
 
@@ -380,17 +414,17 @@ __device__ __forceinline__ uint32_t asm_load_dword_at(const uint8_t* base, uint3
   }
 }
 
-// Wait until this buffer's K loads have landed while the two buffers issued
-// after it (2K loads) stay in flight; output stores issued in between only
-// make the wait stricter, never short.  The buffer registers are in/out
-// operands so no consumer can be scheduled above the wait.
-template <int K>
+// Wait until this buffer's loads have landed while the kYounger loads issued
+// after it (the younger ring buffers) stay in flight; output stores issued in
+// between only make the wait stricter, never short.  The buffer registers are
+// in/out operands so no consumer can be scheduled above the wait.
+template <int kYounger>
 __device__ __forceinline__ void wait_ring(uint32_t (&w)[kRounds]) {
   asm volatile("s_waitcnt vmcnt(%16)"
                : "+v"(w[0]), "+v"(w[1]), "+v"(w[2]), "+v"(w[3]), "+v"(w[4]), "+v"(w[5]), "+v"(w[6]),
                  "+v"(w[7]), "+v"(w[8]), "+v"(w[9]), "+v"(w[10]), "+v"(w[11]), "+v"(w[12]),
                  "+v"(w[13]), "+v"(w[14]), "+v"(w[15])
-               : "n"(2 * K)
+               : "n"(kYounger)
                : "memory");
 }
 
@@ -404,18 +438,14 @@ __device__ __forceinline__ void wait_ring(uint32_t (&w)[kRounds]) {
 // ---------------------------------------------------------------------------
 template <int K>
 __global__ __launch_bounds__(kThreads) void crc32c_fixed_kernel(SpanBatch a) {
+  constexpr int kRing = PRISMDB_RING;
   const uint64_t n = a.n;
   __shared__ uint32_t lds[kLdsWords];
   const uint32_t tid = threadIdx.x;
-  {
-    const uint32_t* src = &a.tabs->stride[0][0];
-    for (uint32_t e = tid; e < (uint32_t)kTabWords; e += kThreads) lds[e] = src[e >> 5];
-    const uint32_t* nib = &a.tabs->lane_nib[0][0][0];
-    for (uint32_t e = tid; e < (uint32_t)kNibWords; e += kThreads) lds[kTabWords + e] = nib[e];
-  }
+  load_tables(lds, a.tabs, tid);
   const uint32_t lane = tid & 63u;
   __syncthreads();
-  const uint32_t* tab = lds + (lane & 31u);
+  const StrideLanes tab = stride_lanes(lane);
   const uint32_t* nibtab = lds + kTabWords + lane;
   const uint64_t wave = rfl(blockIdx.x * kWavesPerGroup + (tid >> 6));
   const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerGroup;
@@ -440,31 +470,45 @@ __global__ __launch_bounds__(kThreads) void crc32c_fixed_kernel(SpanBatch a) {
 #pragma unroll
     for (int j = 1; j < K; ++j) w[j] = asm_load_dword_at<K>(p, off1, j);
   };
-  auto fold = [&](uint64_t k, uint32_t (&w)[kRounds]) {
-    wait_ring<K>(w);  // the two younger buffers (2K loads) may stay in flight
-    uint32_t x = lane >= pk ? w[0] : 0u;
-    x ^= lane == pk ? r0 : 0u;  // initial register enters with body word 0
-    uint32_t acc = x;
+  // Two spans folded together: two independent LDS dependency chains per wave.
+  auto fold2 = [&](uint64_t k, uint32_t (&wa)[kRounds], uint32_t (&wb)[kRounds]) {
+    wait_ring<(kRing - 2) * K>(wa);  // the younger pair may stay in flight
+    wait_ring<(kRing - 2) * K>(wb);
+    uint32_t xa = lane >= pk ? wa[0] : 0u, xb = lane >= pk ? wb[0] : 0u;
+    xa ^= lane == pk ? r0 : 0u;  // initial register enters with body word 0
+    xb ^= lane == pk ? r0 : 0u;
+    uint32_t acc_a = xa, acc_b = xb;
 #pragma unroll
-    for (int j = 1; j < K; ++j) acc = shift256(tab, acc) ^ w[j];
-    const uint32_t crc = wave_xor(realign(nibtab, acc)) ^ kConditioning;
-    if (lane == 0) a.out[wave + k * nwaves] = masked ? mask_crc(crc) : crc;
+    for (int j = 1; j < K; ++j) {
+      acc_a = step256(lds, tab, acc_a, wa[j]);
+      acc_b = step256(lds, tab, acc_b, wb[j]);
+    }
+    const uint32_t va = realign(nibtab, acc_a), vb = realign(nibtab, acc_b);
+    const uint32_t ca = wave_xor(va) ^ kConditioning, cb = wave_xor(vb) ^ kConditioning;
+    const uint64_t ba = wave + k * nwaves, bb = ba + nwaves;
+    if (lane == 0) {
+      a.out[ba] = masked ? mask_crc(ca) : ca;
+      if (bb < n) a.out[bb] = masked ? mask_crc(cb) : cb;
+    }
   };
 
-  uint32_t bA[kRounds], bB[kRounds], bC[kRounds];
-  issue(0, bA);
-  issue(1, bB);
-  for (uint64_t k = 0;; k += 3) {
-    issue(k + 2, bC);
-    fold(k, bA);
-    if (wave + (k + 1) * nwaves >= n) break;
-    issue(k + 3, bA);
-    fold(k + 1, bB);
-    if (wave + (k + 2) * nwaves >= n) break;
-    issue(k + 4, bB);
-    fold(k + 2, bC);
-    if (wave + (k + 3) * nwaves >= n) break;
+  // Ring of kRing span buffers, consumed in pairs; loop unrolled so every
+  // buffer has a static register name.
+  static_assert(kRing % 2 == 0 && kRing >= 4, "the fixed kernel folds spans in pairs, one pair in flight");
+  static_assert((kRing - 2) * K <= 63, "vmcnt is a 6-bit counter");
+  uint32_t ring[kRing][kRounds];
+#pragma unroll
+  for (int d = 0; d < kRing; ++d) issue(d, ring[d]);
+  for (uint64_t k = 0;; k += kRing) {
+#pragma unroll
+    for (int s = 0; s < kRing; s += 2) {
+      fold2(k + s, ring[s], ring[s + 1]);
+      if (wave + (k + s + 2) * nwaves >= n) goto drained;
+      issue(k + s + kRing, ring[s]);
+      issue(k + s + kRing + 1, ring[s + 1]);
+    }
   }
+drained:
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the ring's extra prefetches
 }
 
