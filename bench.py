@@ -146,47 +146,38 @@ def load_pmc_traffic(nblocks: int):
 
 
 def e2e_leg(args, torch, crc32c, dev) -> dict:
-    """Host-resident pipeline: pinned host blocks -> H2D -> CRC -> D2H, 3 streams
-    deep, chunks of 64 MiB (SST-file sized)."""
-    chunk_blocks = 16384  # 64 MiB = one 64 MiB SST's worth of 4 KiB blocks
-    nchunks = 48  # 3 GiB host-resident
-    depth = 3
-    host = torch.empty(chunk_blocks * BLOCK * 8, dtype=torch.uint8, pin_memory=True)  # 512 MiB pinned, reused
-    dbufs = [torch.empty(chunk_blocks * BLOCK, dtype=torch.uint8, device=dev) for _ in range(depth)]
-    douts = [torch.empty(chunk_blocks, dtype=torch.int32, device=dev) for _ in range(depth)]
-    houts = torch.empty(nchunks, chunk_blocks, dtype=torch.int32, pin_memory=True)
-    streams = [torch.cuda.Stream() for _ in range(depth)]
-    tmp = torch.empty(host.numel(), dtype=torch.uint8, device=dev)
+    """Host-resident rate through leveldb_crc32c_batch_host: 4 KiB blocks in
+    host memory streamed H2D -> CRC -> results D2H in 64 MiB chunks, 3 in
+    flight.  Measured for a pinned source (direct DMA) and a pageable one
+    (staged through the engine's pinned ring), next to the plain pinned H2D
+    copy rate of the same bytes.  Never the headline value."""
+    import numpy as np
+
+    nblk = 1 << 19  # 2 GiB of 4 KiB blocks
+    tmp = torch.empty(nblk * BLOCK, dtype=torch.uint8, device=dev)
     crc32c.fill_synthetic(tmp, SEED)
-    host.copy_(tmp)
-    del tmp
+    pinned = tmp.cpu().pin_memory()
+    pageable = pinned.numpy().copy()
+    off = np.arange(nblk, dtype=np.uint64) * BLOCK
+    lens = np.full(nblk, BLOCK, dtype=np.uint32)
+    ref, _ = crc32c.batch_fixed(tmp, BLOCK, BLOCK, nblk)
+    ref = ref.cpu().numpy().view(np.uint32)
+    res = {"bytes": nblk * BLOCK, "chunk": "64 MiB, 3 in flight"}
+    for name, src in (("pinned", pinned), ("pageable", pageable)):
+        crc32c.batch_host(src, off[:16384], lens[:16384])  # warm the ring
+        t0 = time.perf_counter()
+        got, _ = crc32c.batch_host(src, off, lens)
+        t = time.perf_counter() - t0
+        res[name] = round(nblk * BLOCK / t / GIB, 2)
+        res[name + "_bit_exact"] = bool((got == ref).all())
+    d = torch.empty_like(tmp)
     torch.cuda.synchronize()
-
-    def run():
-        for c in range(nchunks):
-            s = streams[c % depth]
-            with torch.cuda.stream(s):
-                src = host[(c % 8) * chunk_blocks * BLOCK:((c % 8) + 1) * chunk_blocks * BLOCK]
-                dbufs[c % depth].copy_(src, non_blocking=True)
-                crc32c.batch_fixed(dbufs[c % depth], BLOCK, BLOCK, chunk_blocks, out=douts[c % depth])
-                houts[c].copy_(douts[c % depth], non_blocking=True)
-        torch.cuda.synchronize()
-
-    run()
     t0 = time.perf_counter()
-    run()
-    t = time.perf_counter() - t0
-    # copy-only ceiling
-    t0 = time.perf_counter()
-    for c in range(nchunks):
-        with torch.cuda.stream(streams[c % depth]):
-            dbufs[c % depth].copy_(host[(c % 8) * chunk_blocks * BLOCK:((c % 8) + 1) * chunk_blocks * BLOCK],
-                                   non_blocking=True)
+    d.copy_(pinned, non_blocking=True)
     torch.cuda.synchronize()
-    tc = time.perf_counter() - t0
-    total = nchunks * chunk_blocks * BLOCK
-    return {"value": round(total / t / GIB, 2), "unit": "GiB/s", "copy_only_h2d": round(total / tc / GIB, 2),
-            "bytes": total, "pipeline": f"{depth} streams x 64 MiB chunks, pinned host, H2D->CRC->D2H"}
+    res["h2d_copy_only"] = round(nblk * BLOCK / (time.perf_counter() - t0) / GIB, 2)
+    res["unit"] = "GiB/s"
+    return res
 
 
 def main() -> int:

@@ -37,6 +37,11 @@ extern "C" {
 
 /* flags */
 #define PRISMDB_CRC32C_MASK 0x1u /* out[i] = crc32c::Mask(crc)  (table/table_builder.cc:196) */
+/* also store the (masked, with MASK) result as 4 LE bytes right after each span,
+ * i.e. seal `contents || type` spans with their trailer in place, as
+ * TableBuilder::WriteRawBlock does (table/table_builder.cc:192-197).  The
+ * buffer must be writable; not combinable with verify (mismatch != NULL). */
+#define PRISMDB_CRC32C_WRITE_TRAILER 0x2u
 
 /* error codes */
 #define PRISMDB_CRC32C_EINVAL (-1)  /* bad argument */
@@ -83,6 +88,20 @@ int leveldb_crc32c_batch_fixed(const void* dev_base, size_t stride, size_t len, 
 int leveldb_crc32c_batch(const void* dev_base, const uint64_t* dev_off, const uint32_t* dev_len,
                          const uint32_t* dev_init, size_t n, uint32_t* dev_out,
                          uint8_t* dev_mismatch, uint32_t flags, void* stream);
+
+/*
+ * Host-resident batch (blocks still in host memory, e.g. SST pages read by
+ * pread during compaction): span i = host_base[off[i], off[i] + len[i]),
+ * offsets sorted ascending, each span (+ its 4-byte trailer when verifying)
+ * at most 64 MiB.  Streams 64 MiB chunks host -> device (through pinned
+ * staging when host_base is pageable; directly when it is pinned/registered)
+ * -> batch kernel -> results back, three chunks in flight on the engine's own
+ * streams.  Synchronous; out/mismatch are host arrays (either may be NULL).
+ * flags: PRISMDB_CRC32C_MASK only.  Uses the current HIP device.
+ */
+int leveldb_crc32c_batch_host(const void* host_base, const uint64_t* off, const uint32_t* len,
+                              const uint32_t* init, size_t n, uint32_t* out, uint8_t* mismatch,
+                              uint32_t flags);
 
 /* Thread-local message for the last non-zero return on this thread. */
 const char* leveldb_crc32c_last_error(void);

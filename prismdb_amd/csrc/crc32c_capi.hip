@@ -214,7 +214,7 @@ int RunBatch(DeviceCtx& ctx, const SpanBatch& base_args, bool desc, bool verify,
   a.role = prismdb::dev::kRoleSpans;
   const bool may_be_long = desc || a.len_c > prismdb::dev::kLongSpan;
   // Fast path: fixed stride, 4-byte aligned, 4..4096-byte multiple-of-4 spans.
-  if (!desc && !verify && a.out != nullptr && a.len_c >= 4 && a.len_c <= 4u * prismdb::dev::kChunkWords &&
+  if (!desc && !verify && a.out != nullptr && (a.flags & prismdb::dev::kFlagWriteTrailer) == 0 && a.len_c >= 4 && a.len_c <= 4u * prismdb::dev::kChunkWords &&
       (a.len_c & 3u) == 0 && (a.stride & 3u) == 0 && (reinterpret_cast<uintptr_t>(a.base) & 3u) == 0 &&
       !g_force_generic) {
     hipError_t e = prismdb::dev::launch_fixed(a, ctx.cus, s);
@@ -257,6 +257,10 @@ int RunBatch(DeviceCtx& ctx, const SpanBatch& base_args, bool desc, bool verify,
 
 }  // namespace
 
+namespace prismdb {
+void SetLastError(const std::string& msg) { t_last_error = msg; }
+}  // namespace prismdb
+
 extern "C" {
 
 int leveldb_crc32c_device_init(int device) {
@@ -279,7 +283,10 @@ int leveldb_crc32c_batch_fixed(const void* dev_base, size_t stride, size_t len, 
   if (nblocks == 0) return 0;
   if (dev_base == nullptr) return Fail(PRISMDB_CRC32C_EINVAL, "dev_base is NULL");
   if (len > 0xFFFFFFFFull) return Fail(PRISMDB_CRC32C_EINVAL, "len must be < 4 GiB");
-  if ((flags & ~PRISMDB_CRC32C_MASK) != 0) return Fail(PRISMDB_CRC32C_EINVAL, "unknown flag bits");
+  if ((flags & ~(PRISMDB_CRC32C_MASK | PRISMDB_CRC32C_WRITE_TRAILER)) != 0)
+    return Fail(PRISMDB_CRC32C_EINVAL, "unknown flag bits");
+  if ((flags & PRISMDB_CRC32C_WRITE_TRAILER) && dev_mismatch != nullptr)
+    return Fail(PRISMDB_CRC32C_EINVAL, "WRITE_TRAILER and verify are exclusive");
   DeviceCtx* ctx = nullptr;
   int rc = GetCtx(&ctx);
   if (rc != 0) return rc;
@@ -301,7 +308,10 @@ int leveldb_crc32c_batch(const void* dev_base, const uint64_t* dev_off, const ui
   if (n == 0) return 0;
   if (dev_base == nullptr || dev_off == nullptr || dev_len == nullptr)
     return Fail(PRISMDB_CRC32C_EINVAL, "dev_base/dev_off/dev_len must be non-NULL");
-  if ((flags & ~PRISMDB_CRC32C_MASK) != 0) return Fail(PRISMDB_CRC32C_EINVAL, "unknown flag bits");
+  if ((flags & ~(PRISMDB_CRC32C_MASK | PRISMDB_CRC32C_WRITE_TRAILER)) != 0)
+    return Fail(PRISMDB_CRC32C_EINVAL, "unknown flag bits");
+  if ((flags & PRISMDB_CRC32C_WRITE_TRAILER) && dev_mismatch != nullptr)
+    return Fail(PRISMDB_CRC32C_EINVAL, "WRITE_TRAILER and verify are exclusive");
   DeviceCtx* ctx = nullptr;
   int rc = GetCtx(&ctx);
   if (rc != 0) return rc;

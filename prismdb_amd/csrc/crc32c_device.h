@@ -11,6 +11,7 @@ constexpr uint32_t kPolyReflected = 0x82F63B78u;
 constexpr uint32_t kConditioning = 0xFFFFFFFFu;  // util/crc32c.cc:246
 constexpr uint32_t kMaskDelta = 0xa282ead8u;     // util/crc32c.h:22
 constexpr uint32_t kFlagMask = 0x1u;             // == PRISMDB_CRC32C_MASK
+constexpr uint32_t kFlagWriteTrailer = 0x2u;     // == PRISMDB_CRC32C_WRITE_TRAILER
 
 constexpr int kWave = 64;
 constexpr int kWavesPerGroup = 16;                 // 1024-thread workgroup, one per CU

@@ -65,6 +65,16 @@ __device__ __forceinline__ uint32_t feed_byte(uint32_t r, uint32_t byte) {
   return r;
 }
 
+// The caller owns the span's trailer bytes when it asks for them to be written
+// (TableBuilder::WriteRawBlock, table/table_builder.cc:196).
+__device__ __forceinline__ void store_le32(const uint8_t* p, uint32_t v) {
+  uint8_t* q = const_cast<uint8_t*>(p);
+  q[0] = (uint8_t)v;
+  q[1] = (uint8_t)(v >> 8);
+  q[2] = (uint8_t)(v >> 16);
+  q[3] = (uint8_t)(v >> 24);
+}
+
 __device__ __forceinline__ uint32_t mask_crc(uint32_t c) { return ((c << 17) | (c >> 15)) + kMaskDelta; }
 __device__ __forceinline__ uint32_t unmask_crc(uint32_t m) {
   const uint32_t r = m - kMaskDelta;
@@ -361,7 +371,9 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
         const uint32_t crc = r ^ kConditioning;
         const uint64_t b = wave + t0.k * nwaves;
         if (lane == 0) {
-          if (a.out != nullptr) a.out[b] = (a.flags & kFlagMask) ? mask_crc(crc) : crc;
+          const uint32_t res = (a.flags & kFlagMask) ? mask_crc(crc) : crc;
+          if (a.out != nullptr) a.out[b] = res;
+          if (a.flags & kFlagWriteTrailer) store_le32(g.p + g.len, res);
           if (kVerify && a.mismatch != nullptr) {
             const uint32_t stored = readlane(ecur, 6) | (readlane(ecur, 7) << 8) |
                                     (readlane(ecur, 8) << 16) | (readlane(ecur, 9) << 24);
@@ -567,10 +579,12 @@ __global__ __launch_bounds__(256) void crc32c_combine_kernel(SpanBatch a, SplitW
       r = y ^ ws.seg_out[first + s] ^ kConditioning;
     }
     const uint32_t crc = r ^ kConditioning;
-    if (a.out != nullptr) a.out[span] = (a.flags & kFlagMask) ? mask_crc(crc) : crc;
+    const uint32_t res = (a.flags & kFlagMask) ? mask_crc(crc) : crc;
+    if (a.out != nullptr) a.out[span] = res;
+    const uint64_t off = kDesc ? a.off[span] : span * a.stride;
+    const uint32_t len = kDesc ? a.len[span] : a.len_c;
+    if (a.flags & kFlagWriteTrailer) store_le32(a.base + off + len, res);
     if (kVerify && a.mismatch != nullptr) {
-      const uint64_t off = kDesc ? a.off[span] : span * a.stride;
-      const uint32_t len = kDesc ? a.len[span] : a.len_c;
       const uint8_t* t = a.base + off + len;
       const uint32_t stored = (uint32_t)t[0] | ((uint32_t)t[1] << 8) | ((uint32_t)t[2] << 16) |
                               ((uint32_t)t[3] << 24);

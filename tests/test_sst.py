@@ -1,0 +1,101 @@
+"""SST layout walker (host, CPU) and whole-table verify / seal on the device.
+
+Pinned by the SST written and re-verified by the reference TableBuilder
+(tests/golden/sst_small.*, oracle/sst_fixture.cc)."""
+import numpy as np
+import pytest
+
+
+def test_block_spans_match_reference_table(native, golden):
+    from prismdb_amd import sst
+
+    off, ln, kind = sst.block_spans(golden["sst_bytes"])
+    blocks = golden["sst"]["blocks"]
+    got = [(int(o), int(n) - 1, sst.KIND_NAMES[int(k)]) for o, n, k in zip(off, ln, kind)]
+    want = [(b["offset"], b["size"], b["kind"]) for b in blocks]
+    assert got == want
+
+
+@pytest.mark.parametrize("damage,msg", [
+    (lambda f: f[:-1] + bytes([f[-1] ^ 1]), "Corruption: not an sstable (bad magic number)"),
+    (lambda f: f[:40], "Corruption: file is too short to be an sstable"),
+    (lambda f: f[:-48 - 1000] + f[-48:], "Corruption: truncated block read"),
+])
+def test_block_spans_layout_errors(native, golden, damage, msg):
+    from prismdb_amd import sst
+
+    with pytest.raises(sst.SstCorruption, match=msg.replace("(", r"\(").replace(")", r"\)")):
+        sst.block_spans(damage(golden["sst_bytes"]))
+
+
+def test_block_spans_index_checksum_checked_first(native, golden):
+    from prismdb_amd import sst
+
+    f = bytearray(golden["sst_bytes"])
+    idx = [b for b in golden["sst"]["blocks"] if b["kind"] == "index"][0]
+    f[idx["offset"] + 3] ^= 0x10
+    with pytest.raises(sst.SstCorruption, match="block checksum mismatch"):
+        sst.block_spans(bytes(f))
+
+
+@pytest.mark.gpu
+def test_verify_tables_device(native, golden):
+    """One device batch over several tables; one corrupted data block, one
+    corrupted metaindex trailer, one table with a broken footer."""
+    from prismdb_amd import sst
+
+    clean = golden["sst_bytes"]
+    blocks = golden["sst"]["blocks"]
+    bad_data = bytearray(clean)
+    bad_data[blocks[9]["offset"] + 17] ^= 0x80
+    meta = [b for b in blocks if b["kind"] == "metaindex"][0]
+    bad_meta = bytearray(clean)
+    bad_meta[meta["offset"] + meta["size"] + 1] ^= 0x04
+    no_magic = clean[:-1] + bytes([clean[-1] ^ 0xFF])
+    res = sst.verify_tables([clean, bytes(bad_data), clean, bytes(bad_meta), no_magic])
+    assert res.table_errors == ["", "", "", "", "Corruption: not an sstable (bad magic number)"]
+    bad = [(b.table, b.kind, b.offset) for b in res.bad_blocks()]
+    assert bad == [(1, "data", blocks[9]["offset"]), (3, "metaindex", meta["offset"])]
+    assert all(b.status == sst.MISMATCH for b in res.bad_blocks())
+    assert len(res.blocks) == 4 * len(blocks)
+
+
+@pytest.mark.gpu
+def test_seal_blocks_reproduces_reference_trailers(native, golden):
+    """Zero every CRC in the reference SST, reseal all blocks in one device
+    call: the file is byte-identical to what TableBuilder wrote."""
+    import torch
+    from prismdb_amd import sst
+
+    f = np.frombuffer(golden["sst_bytes"], dtype=np.uint8).copy()
+    blocks = golden["sst"]["blocks"]
+    for b in blocks:
+        f[b["offset"] + b["size"] + 1:b["offset"] + b["size"] + 5] = 0
+    dev = torch.device("cuda", 0)
+    buf = torch.from_numpy(f).to(dev)
+    off = torch.tensor([b["offset"] for b in blocks], dtype=torch.int64, device=dev)
+    size = torch.tensor([b["size"] for b in blocks], dtype=torch.int32, device=dev)
+    masked = sst.seal_blocks(buf, off, size)
+    torch.cuda.synchronize()
+    assert buf.cpu().numpy().tobytes() == golden["sst_bytes"]
+    assert [int(x) & 0xFFFFFFFF for x in masked.tolist()] == [b["masked_crc"] for b in blocks]
+
+
+@pytest.mark.gpu
+def test_seal_long_block_split_path(native, oracle):
+    """Trailer written by the combine kernel for a span above the split threshold."""
+    import torch
+    from prismdb_amd import crc32c, sst
+
+    n = 300000
+    host = oracle.synth(n + 16, 0x5EED000B)
+    host[n] = 1  # type byte
+    dev = torch.device("cuda", 0)
+    buf = torch.from_numpy(host.copy()).to(dev)
+    sst.seal_blocks(buf, torch.tensor([0], dtype=torch.int64, device=dev),
+                    torch.tensor([n], dtype=torch.int32, device=dev))
+    torch.cuda.synchronize()
+    out = buf.cpu().numpy()
+    want = oracle.mask(oracle.value(host[:n + 1].tobytes()))
+    assert int.from_bytes(out[n + 1:n + 5].tobytes(), "little") == want
+    assert (out[:n + 1] == host[:n + 1]).all() and (out[n + 5:] == host[n + 5:]).all()
