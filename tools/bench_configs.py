@@ -1,0 +1,118 @@
+#!/usr/bin/env python3
+"""Secondary workloads of BASELINE.json (the headline is bench.py).
+
+    python tools/bench_configs.py [--reps 5]
+
+Prints one JSON object with, per workload, the mean kernel-sequence time
+(HIP events on the launch stream), payload GiB/s and the HBM roofline fraction
+of the algorithmic bytes (fixed L+4; variable L+4+12; verify
+L+4+1 per span):
+  config3_mixed      spans of 1/4/16/64 KiB (uniform, seed 0x5EED0003) packed back to back, ~16 GiB
+  sst_fixed          3988-B spans (YCSB data block + type byte) at stride 3992, 16 Mi spans (~62.4 GiB)
+  sst_desc           same spans through descriptors + one 486 977-B index span per 16 811 (split path)
+  verify_4k          ReadBlock-verify of 16 Mi x (4092 + type... ) 4 KiB spans with stored trailers
+  adversarial        random lengths 0..70 000 at random byte offsets (2 Mi spans over 16 GiB)
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+GIB = float(1 << 30)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=5)
+    args = ap.parse_args()
+    import numpy as np
+    import torch
+    from prismdb_amd import crc32c
+
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.current_stream()
+
+    def timed(fn, reps):
+        ts = []
+        fn()
+        for _ in range(reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            fn()
+            e1.record(stream)
+            e1.synchronize()
+            ts.append(e0.elapsed_time(e1) / 1e3)
+        return statistics.median(ts)
+
+    res = {}
+
+    def report(name, t, payload, algo, n):
+        res[name] = {"spans": n, "payload_GiB": round(payload / GIB, 2), "ms": round(t * 1e3, 3),
+                     "GiB/s": round(payload / t / GIB, 1), "algo_GB/s": round(algo / t / 1e9, 1),
+                     "roofline_frac": round(algo / t / 8e12, 4)}
+
+    # one 64 GiB buffer serves every workload
+    buf = torch.empty(64 << 30, dtype=torch.uint8, device=dev)
+    crc32c.fill_synthetic(buf, 0x5EED0001)
+
+    # config 3: mixed sizes
+    rng = np.random.default_rng(0x5EED0003)
+    lens = rng.choice([1024, 4096, 16384, 65536], size=(16 << 30) // 21760).astype(np.int64)
+    off = np.concatenate([[0], np.cumsum(lens)[:-1]])
+    d_off, d_len = torch.from_numpy(off).to(dev), torch.from_numpy(lens.astype(np.int32)).to(dev)
+    out = torch.empty(len(lens), dtype=torch.int32, device=dev)
+    t = timed(lambda: crc32c.batch(buf, d_off, d_len, out=out), args.reps)
+    report("config3_mixed", t, lens.sum(), lens.sum() + 16 * len(lens), len(lens))
+    del d_off, d_len, out
+
+    # SST-shaped, fixed stride
+    n = 1 << 24
+    out = torch.empty(n, dtype=torch.int32, device=dev)
+    t = timed(lambda: crc32c.batch_fixed(buf, 3992, 3988, n, out=out, mask=True), args.reps)
+    report("sst_fixed", t, n * 3988, n * (3988 + 4), n)
+
+    # SST-shaped, descriptors, with index spans (one per 64 MiB SST: 16 811 data spans)
+    per = 16811
+    files = n // (per + 122)
+    offs, lns = [], []
+    pos = 0
+    for _ in range(files):
+        offs.append(pos + np.arange(per, dtype=np.int64) * 3992)
+        lns.append(np.full(per, 3988, dtype=np.int64))
+        pos += per * 3992
+        offs.append(np.array([pos], dtype=np.int64))
+        lns.append(np.array([486977], dtype=np.int64))
+        pos += 486977 + 4 + 3
+        pos = (pos + 7) & ~7
+    off = np.concatenate(offs)
+    lens = np.concatenate(lns)
+    assert off[-1] + lens[-1] + 4 <= buf.numel()
+    d_off, d_len = torch.from_numpy(off).to(dev), torch.from_numpy(lens.astype(np.int32)).to(dev)
+    out2 = torch.empty(len(off), dtype=torch.int32, device=dev)
+    t = timed(lambda: crc32c.batch(buf, d_off, d_len, out=out2, mask=True), args.reps)
+    report("sst_desc", t, lens.sum(), lens.sum() + 16 * len(lens), len(lens))
+    del d_off, d_len, out2
+
+    # verify 4 KiB spans (fixed stride 4096, span 4092 B, trailer in the last 4 B)
+    out = torch.empty(n, dtype=torch.int32, device=dev)
+    mm = torch.empty(n, dtype=torch.uint8, device=dev)
+    t = timed(lambda: crc32c.batch_fixed(buf, 4096, 4092, n, out=out, mismatch=mm, verify=True), args.reps)
+    report("verify_4k", t, n * 4092, n * (4092 + 4 + 1 + 4), n)
+
+    # adversarial
+    m = 2 << 20
+    lens = rng.integers(0, 70000, size=m).astype(np.int64)
+    off = np.sort(rng.integers(0, (16 << 30) - 70001, size=m)).astype(np.int64)
+    d_off, d_len = torch.from_numpy(off).to(dev), torch.from_numpy(lens.astype(np.int32)).to(dev)
+    out3 = torch.empty(m, dtype=torch.int32, device=dev)
+    t = timed(lambda: crc32c.batch(buf, d_off, d_len, out=out3), args.reps)
+    report("adversarial", t, lens.sum(), lens.sum() + 16 * m, m)
+
+    print(json.dumps({"reps": args.reps, "results": res}, indent=1))
+
+
+if __name__ == "__main__":
+    main()
