@@ -31,6 +31,9 @@
 
 #include "crc32c_device.h"
 
+#ifndef PRISMDB_SPAN_V1
+#define PRISMDB_SPAN_V1 0  // 1: previous generic kernel (compiler-managed loads), for A/B runs
+#endif
 #ifndef PRISMDB_RING
 #define PRISMDB_RING 4  // span buffers in the fixed kernel's prefetch ring (even)
 #endif
@@ -441,6 +444,314 @@ __device__ __forceinline__ void wait_ring(uint32_t (&w)[kRounds]) {
 }
 
 // ---------------------------------------------------------------------------
+// Generic span kernel, v2: two independent span streams per wave folded in
+// lockstep (stream 0 takes the wave's even span ordinals, stream 1 the odd
+// ones), every load an inline-asm BUFFER load issued two tasks ahead and
+// retired by a counted vmcnt.  A task is one 4 KiB chunk of one span and
+// always issues exactly 17 loads (16 body dwords + 1 edge byte): loads outside
+// the span hit the buffer range check and return 0 without touching memory,
+// which provides the right-aligned zero padding of chunk 0 and lets invalid or
+// skipped tasks run through the same code.
+// ---------------------------------------------------------------------------
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// Uniform-address load through the scalar cache (constant address space).
+template <typename T>
+__device__ __forceinline__ T const_load(const T* p, uint64_t i) {
+  typedef const __attribute__((address_space(4))) T CT;
+  return ((CT*)p)[i];
+}
+
+__device__ __forceinline__ u32x4 buffer_rsrc(const uint8_t* p, uint32_t bytes) {
+  const uint64_t a = reinterpret_cast<uint64_t>(p);
+  u32x4 r;
+  // wave-uniform by construction; readfirstlane puts it in SGPRs for the "s" operand
+  r.x = rfl((uint32_t)a);
+  r.y = rfl((uint32_t)(a >> 32) & 0xffffu);  // stride 0: raw buffer
+  r.z = rfl(bytes);                          // num_records: offsets >= bytes read as 0
+  r.w = 0x00020000u;                         // gfx950 raw-buffer word 3 (cdna_hip_programming.md T8)
+  return r;
+}
+
+template <int kImm>
+__device__ __forceinline__ uint32_t buf_dword(u32x4 rs, uint32_t voff) {
+  uint32_t r;
+#if PRISMDB_NT_LOADS
+  asm volatile("buffer_load_dword %0, %1, %2, 0 offen offset:%3 nt" : "=v"(r) : "v"(voff), "s"(rs), "n"(kImm));
+#else
+  asm volatile("buffer_load_dword %0, %1, %2, 0 offen offset:%3" : "=v"(r) : "v"(voff), "s"(rs), "n"(kImm));
+#endif
+  return r;
+}
+
+__device__ __forceinline__ uint32_t buf_ubyte(u32x4 rs, uint32_t voff) {
+  uint32_t r;
+  asm volatile("buffer_load_ubyte %0, %1, %2, 0 offen" : "=v"(r) : "v"(voff), "s"(rs));
+  return r;
+}
+
+template <int J>
+__device__ __forceinline__ void buf_round(uint32_t (&w)[kRounds], u32x4 rs, uint32_t voff) {
+  w[J] = buf_dword<256 * J>(rs, voff);
+}
+
+// Wait for a buffer (16 body words + edge) with kYounger loads left in flight.
+template <int kYounger>
+__device__ __forceinline__ void wait_task(uint32_t (&w)[kRounds], uint32_t& e) {
+  wait_ring<kYounger>(w);
+  asm volatile("" : "+v"(e));
+}
+
+// Wave-uniform task (span ordinal q, chunk c); the span's geometry is
+// recomputed from (p, len) when needed to keep the SGPR footprint small.
+struct Task {
+  const uint8_t* p;
+  uint64_t q;
+  uint32_t len, init;
+  uint32_t c;
+  bool valid, skip;
+  __device__ uint32_t h() const {
+    const uint32_t x = (4u - ((uint32_t)(uintptr_t)p & 3u)) & 3u;
+    return x < len ? x : len;
+  }
+  __device__ uint32_t W() const { return (len - h()) >> 2; }
+  __device__ uint32_t t() const { return (len - h()) & 3u; }
+  __device__ uint32_t nch() const {
+    const uint32_t w = W();
+    return w ? (w + kChunkWords - 1u) / kChunkWords : 1u;
+  }
+  __device__ uint32_t pad() const { return nch() * kChunkWords - W(); }
+};
+
+template <bool kDesc, bool kVerify>
+__global__ __launch_bounds__(kThreads) void crc32c_span2_kernel(SpanBatch a) {
+  uint64_t n = a.n;
+  if (a.n_dev != nullptr) {
+    const uint64_t m = *a.n_dev;
+    n = m < n ? m : n;
+  }
+  uint32_t skip_above = a.skip_above;
+  if (a.overflow != nullptr && *a.overflow != 0u) {
+    if (a.role == kRoleSegments) n = 0;
+    else skip_above = 0xFFFFFFFFu;
+  }
+  if (n == 0) return;
+
+  __shared__ uint32_t lds[kLdsWords];
+  const uint32_t tid = threadIdx.x;
+  load_tables(lds, a.tabs, tid);
+  const uint32_t lane = tid & 63u;
+  __syncthreads();
+  const StrideLanes tab = stride_lanes(lane);
+  const uint32_t* nibtab = lds + kTabWords + lane;
+  const uint64_t wave = rfl(blockIdx.x * kWavesPerGroup + (tid >> 6));
+  const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerGroup;
+  if (wave >= n) return;
+
+  // span b of stream s, ordinal q: b = wave + (2q + s) * nwaves
+  auto span_of = [&](int s, uint64_t q) -> uint64_t { return wave + (2 * q + (uint64_t)s) * nwaves; };
+  // Descriptors come through the scalar cache (constant address space), one
+  // span ahead per stream: a vector load here would make the compiler wait
+  // vmcnt(0) and drain the asm load ring.
+  struct Desc {
+    uint64_t off;
+    uint32_t len, init;
+  };
+  auto read_desc = [&](int s, uint64_t q) -> Desc {
+    Desc d{0, 0, 0};
+    const uint64_t b = span_of(s, q);
+    if (b < n) {
+      if (kDesc) {
+        d.off = const_load(a.off, b);
+        d.len = const_load(a.len, b);
+        d.init = a.init != nullptr ? const_load(a.init, b) : 0u;
+      } else {
+        d.off = b * a.stride;
+        d.len = a.len_c;
+        d.init = a.init_c;
+      }
+    }
+    return d;
+  };
+  auto make_task = [&](int s, uint64_t q, const Desc& d) -> Task {
+    Task t;
+    t.q = q;
+    t.c = 0;
+    t.valid = span_of(s, q) < n;
+    t.p = a.base + d.off;
+    t.len = d.len;
+    t.init = d.init;
+    t.skip = !t.valid || d.len > skip_above;
+    return t;
+  };
+  Desc pend[2];           // descriptor of the span after each stream's newest task
+  uint64_t newest[2] = {0, 0};
+  bool refill[2] = {false, false};
+  auto next_task = [&](int s, const Task& t) -> Task {
+    if (t.c + 1 < t.nch()) {
+      Task u = t;
+      u.c = t.c + 1;
+      return u;
+    }
+    Task u = make_task(s, t.q + 1, pend[s]);
+    u.valid = u.valid && t.valid;
+    u.skip = u.skip || !u.valid;
+    newest[s] = t.q + 1;
+    refill[s] = true;
+    return u;
+  };
+  auto refill_desc = [&]() {  // after both streams took theirs: the scalar wait covers only older loads
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      if (refill[s]) {
+        refill[s] = false;
+        pend[s] = read_desc(s, newest[s] + 1);
+      }
+    }
+  };
+  // 17 loads, always.
+  auto issue = [&](const Task& t, uint32_t (&w)[kRounds], uint32_t& e) {
+    const bool live = !t.skip;
+    const uint32_t h = t.h(), W = t.W(), tl = t.t(), nch = t.nch(), pad = nch * kChunkWords - W;
+    u32x4 rb = buffer_rsrc(t.p + h, live ? 4u * W : 0u);
+    u32x4 re = buffer_rsrc(t.p, live ? t.len + (kVerify ? 4u : 0u) : 0u);
+    // The descriptors were just written by v_readfirstlane (VALU -> SGPR) and
+    // the buffer loads below read them from inside asm, where hipcc inserts no
+    // wait states: 5 are required (cdna_hip_programming.md 5.7 item 2).
+    asm volatile("s_nop 4" : "+s"(rb), "+s"(re));
+    const int32_t i0 = (int32_t)(t.c * kChunkWords + lane) - (int32_t)pad;
+    if (t.c == 0 && pad != 0) {
+      // chunk 0: offsets may be negative; give every round its own voffset so
+      // the range check sees the wrapped (huge) value, never a wrapped sum
+#pragma unroll
+      for (int j = 0; j < kRounds; ++j) w[j] = buf_dword<0>(rb, (uint32_t)(i0 + 64 * j) * 4u);
+    } else {
+      const uint32_t v = (uint32_t)i0 * 4u;
+      buf_round<0>(w, rb, v);  buf_round<1>(w, rb, v);  buf_round<2>(w, rb, v);  buf_round<3>(w, rb, v);
+      buf_round<4>(w, rb, v);  buf_round<5>(w, rb, v);  buf_round<6>(w, rb, v);  buf_round<7>(w, rb, v);
+      buf_round<8>(w, rb, v);  buf_round<9>(w, rb, v);  buf_round<10>(w, rb, v); buf_round<11>(w, rb, v);
+      buf_round<12>(w, rb, v); buf_round<13>(w, rb, v); buf_round<14>(w, rb, v); buf_round<15>(w, rb, v);
+    }
+    const bool first = t.c == 0, last = t.c + 1 == nch;
+    uint32_t eoff = 0xFFFFFFFFu;
+    if (first && lane < h) eoff = lane;
+    if (last && lane >= 3u && lane < 3u + tl) eoff = h + 4u * W + (lane - 3u);
+    if (kVerify && last && lane >= 6u && lane < 10u) eoff = t.len + (lane - 6u);
+    e = buf_ubyte(re, eoff);
+  };
+
+  // Per-stream chain state.
+  uint32_t acc[2] = {0u, 0u}, r[2] = {0u, 0u};
+
+  // Start of a chunk: head bytes and the initial-register injection (chunk 0).
+  auto begin = [&](int s, const Task& t, uint32_t (&w)[kRounds], uint32_t e) {
+    if (t.c == 0) {
+      const uint32_t h = t.h(), W = t.W();
+      uint32_t rr = t.init ^ kConditioning;
+      for (uint32_t qb = 0; qb < h; ++qb) rr = feed_byte(rr, readlane(e, qb));
+      r[s] = rr;
+      acc[s] = 0u;
+      if (W) {
+        const uint32_t pad = t.nch() * kChunkWords - W;
+        const uint32_t inj = lane == (pad & 63u) ? rr : 0u;  // enters with body word 0
+        switch (pad >> 6) {
+#define PRISMDB_INJ(J) \
+  case J:              \
+    w[J] ^= inj;       \
+    break;
+          PRISMDB_INJ(0) PRISMDB_INJ(1) PRISMDB_INJ(2) PRISMDB_INJ(3) PRISMDB_INJ(4) PRISMDB_INJ(5)
+          PRISMDB_INJ(6) PRISMDB_INJ(7) PRISMDB_INJ(8) PRISMDB_INJ(9) PRISMDB_INJ(10) PRISMDB_INJ(11)
+          PRISMDB_INJ(12) PRISMDB_INJ(13) PRISMDB_INJ(14) PRISMDB_INJ(15)
+#undef PRISMDB_INJ
+          default:
+            break;
+        }
+      }
+    }
+  };
+  // End of a span: tail bytes, conditioning, outputs.
+  auto finish = [&](int s, const Task& t, uint32_t e, uint32_t body) {
+    uint32_t rr = t.W() ? body : r[s];
+    const uint32_t tl = t.t();
+    for (uint32_t qb = 0; qb < tl; ++qb) rr = feed_byte(rr, readlane(e, 3u + qb));
+    const uint32_t crc = rr ^ kConditioning;
+    const uint64_t b = span_of(s, t.q);
+    if (lane == 0) {
+      const uint32_t res = (a.flags & kFlagMask) ? mask_crc(crc) : crc;
+      if (a.out != nullptr) a.out[b] = res;
+      if (a.flags & kFlagWriteTrailer) store_le32(t.p + t.len, res);
+      if (kVerify && a.mismatch != nullptr) {
+        const uint32_t stored = readlane(e, 6) | (readlane(e, 7) << 8) | (readlane(e, 8) << 16) |
+                                (readlane(e, 9) << 24);
+        a.mismatch[b] = crc != unmask_crc(stored) ? 1 : 0;
+      }
+    }
+  };
+  // Fold the pair (stream 0 task tx in wx, stream 1 task ty in wy).
+  auto fold = [&](const Task& tx, uint32_t (&wx)[kRounds], uint32_t ex, const Task& ty,
+                  uint32_t (&wy)[kRounds], uint32_t ey) {
+    if (!tx.skip) begin(0, tx, wx, ex);
+    if (!ty.skip) begin(1, ty, wy, ey);
+    uint32_t ax = acc[0], ay = acc[1];
+#pragma unroll
+    for (int j = 0; j < kRounds; ++j) {
+      ax = step256(lds, tab, ax, wx[j]);
+      ay = step256(lds, tab, ay, wy[j]);
+    }
+    acc[0] = ax;
+    acc[1] = ay;
+    const bool endx = !tx.skip && tx.c + 1 == tx.nch(), endy = !ty.skip && ty.c + 1 == ty.nch();
+    if (endx && endy) {
+      const uint32_t vx = realign(nibtab, ax), vy = realign(nibtab, ay);
+      const uint32_t bx = wave_xor(vx), by = wave_xor(vy);
+      finish(0, tx, ex, bx);
+      finish(1, ty, ey, by);
+    } else if (endx) {
+      finish(0, tx, ex, wave_xor(realign(nibtab, ax)));
+    } else if (endy) {
+      finish(1, ty, ey, wave_xor(realign(nibtab, ay)));
+    }
+  };
+
+  // Ring: two slots x two streams, compile-time slot indices (loop unrolled
+  // over the slots, as in the fixed kernel) so no buffer register is copied
+  // across the back-edge while its loads are in flight.  Fold slot `sl` while
+  // the other slot's two tasks are in flight, then refill slot `sl`.
+  Task tk[2][2];
+  uint32_t wb[2][2][kRounds];
+  uint32_t eb[2][2];
+  tk[0][0] = make_task(0, 0, read_desc(0, 0));
+  tk[0][1] = make_task(1, 0, read_desc(1, 0));
+  pend[0] = read_desc(0, 1);
+  pend[1] = read_desc(1, 1);
+  tk[1][0] = next_task(0, tk[0][0]);
+  tk[1][1] = next_task(1, tk[0][1]);
+  refill_desc();
+#pragma unroll
+  for (int sl = 0; sl < 2; ++sl) {
+    issue(tk[sl][0], wb[sl][0], eb[sl][0]);
+    issue(tk[sl][1], wb[sl][1], eb[sl][1]);
+  }
+  constexpr int kYounger = 2 * (kRounds + 1);  // the other slot's two tasks
+  for (;;) {
+#pragma unroll
+    for (int sl = 0; sl < 2; ++sl) {
+      wait_task<kYounger>(wb[sl][0], eb[sl][0]);
+      wait_task<kYounger>(wb[sl][1], eb[sl][1]);
+      fold(tk[sl][0], wb[sl][0], eb[sl][0], tk[sl][1], wb[sl][1], eb[sl][1]);
+      if (!tk[sl ^ 1][0].valid && !tk[sl ^ 1][1].valid) goto drained;
+      tk[sl][0] = next_task(0, tk[sl ^ 1][0]);
+      tk[sl][1] = next_task(1, tk[sl ^ 1][1]);
+      refill_desc();
+      issue(tk[sl][0], wb[sl][0], eb[sl][0]);
+      issue(tk[sl][1], wb[sl][1], eb[sl][1]);
+    }
+  }
+drained:
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// ---------------------------------------------------------------------------
 // Fixed-geometry fast path: every span is len bytes at base + i*stride with
 // base, stride and len multiples of 4 and len <= 4 KiB, so a span is K rounds
 // (K = ceil(len/256), a template parameter) with no head/tail bytes and the
@@ -597,13 +908,19 @@ __global__ __launch_bounds__(256) void crc32c_combine_kernel(SpanBatch a, SplitW
 // Host-side launchers (called from crc32c_capi.cc through crc32c_device.h).
 // ---------------------------------------------------------------------------
 hipError_t launch_span(const SpanBatch& a, bool desc, bool verify, int grid, hipStream_t s) {
+#if PRISMDB_SPAN_V1
+#define PRISMDB_SPAN crc32c_span_kernel
+#else
+#define PRISMDB_SPAN crc32c_span2_kernel
+#endif
   if (desc) {
-    if (verify) crc32c_span_kernel<true, true><<<grid, kThreads, 0, s>>>(a);
-    else crc32c_span_kernel<true, false><<<grid, kThreads, 0, s>>>(a);
+    if (verify) PRISMDB_SPAN<true, true><<<grid, kThreads, 0, s>>>(a);
+    else PRISMDB_SPAN<true, false><<<grid, kThreads, 0, s>>>(a);
   } else {
-    if (verify) crc32c_span_kernel<false, true><<<grid, kThreads, 0, s>>>(a);
-    else crc32c_span_kernel<false, false><<<grid, kThreads, 0, s>>>(a);
+    if (verify) PRISMDB_SPAN<false, true><<<grid, kThreads, 0, s>>>(a);
+    else PRISMDB_SPAN<false, false><<<grid, kThreads, 0, s>>>(a);
   }
+#undef PRISMDB_SPAN
   return hipGetLastError();
 }
 

@@ -20,8 +20,8 @@ sys.path.insert(0, ROOT)
 VDIR = os.path.join(ROOT, "tools", "_build", "variants")
 
 VARIANTS = {
-    "ring4_nt1": {"PRISMDB_RING": 4, "PRISMDB_NT_LOADS": 1},
-    "ring4_nt0": {"PRISMDB_RING": 4, "PRISMDB_NT_LOADS": 0},
+    "base": {"PRISMDB_RING": 4, "PRISMDB_NT_LOADS": 1},
+    "span_v1": {"PRISMDB_SPAN_V1": 1},
 }
 
 
@@ -33,6 +33,7 @@ def do_build(names):
 
 
 def do_run(args, names):
+    import numpy as np
     import torch
 
     from prismdb_amd import crc32c  # product lib: data generator
@@ -42,6 +43,7 @@ def do_run(args, names):
     buf = torch.empty(nblk * 4096, dtype=torch.uint8, device=dev)
     crc32c.fill_synthetic(buf, 0x5EED0001)
     stream = torch.cuda.current_stream()
+    sp = ctypes.c_void_p(stream.cuda_stream)
     libs = {}
     for name in names:
         lib = ctypes.CDLL(os.path.join(VDIR, f"lib_{name}.so"), mode=os.RTLD_LOCAL)
@@ -49,36 +51,51 @@ def do_run(args, names):
         f.restype = ctypes.c_int
         f.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_uint32,
                       ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]
-        libs[name] = f
-    outs = {n: torch.empty(nblk, dtype=torch.int32, device=dev) for n in names}
+        g = lib.leveldb_crc32c_batch
+        g.restype = ctypes.c_int
+        g.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]
+        libs[name] = (f, g)
+    out = torch.empty(nblk, dtype=torch.int32, device=dev)
+    mm = torch.empty(nblk, dtype=torch.uint8, device=dev)
+    off4k = torch.arange(nblk, dtype=torch.int64, device=dev) * 4096
+    len4k = torch.full((nblk,), 4096, dtype=torch.int32, device=dev)
+    rng = np.random.default_rng(0x5EED0003)
+    ml = rng.choice([1024, 4096, 16384, 65536], size=(args.gib << 30) // 21760 // 2).astype(np.int64)
+    mo = np.concatenate([[0], np.cumsum(ml)[:-1]])
+    moff, mlen = torch.from_numpy(mo).to(dev), torch.from_numpy(ml.astype(np.int32)).to(dev)
+    work = {
+        "fixed4k": (lambda n: libs[n][0](buf.data_ptr(), 4096, 4096, nblk, 0, out.data_ptr(), None, 0, sp),
+                    nblk * 4100),
+        "desc4k": (lambda n: libs[n][1](buf.data_ptr(), off4k.data_ptr(), len4k.data_ptr(), None, nblk,
+                                        out.data_ptr(), None, 0, sp), nblk * 4112),
+        "verify4k": (lambda n: libs[n][0](buf.data_ptr(), 4096, 4092, nblk, 0, out.data_ptr(), mm.data_ptr(), 0,
+                                          sp), nblk * 4105),
+        "mixed": (lambda n: libs[n][1](buf.data_ptr(), moff.data_ptr(), mlen.data_ptr(), None, len(ml),
+                                       out.data_ptr(), None, 0, sp), int(ml.sum()) + 16 * len(ml)),
+    }
 
-    def call(n):
-        rc = libs[n](buf.data_ptr(), 4096, 4096, nblk, 0, outs[n].data_ptr(), None, 0,
-                     ctypes.c_void_p(stream.cuda_stream))
-        assert rc == 0, (n, rc)
-
-    def timed(n):
+    def timed(fn, n):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(stream)
-        call(n)
+        rc = fn(n)
         e1.record(stream)
         e1.synchronize()
+        assert rc == 0, (n, rc)
         return e0.elapsed_time(e1) / 1e3
 
-    for n in names:
-        timed(n)
-    ref = outs[names[0]]
-    same = {n: bool(torch.equal(outs[n], ref)) for n in names}
-    res = {n: [] for n in names}
-    for _ in range(args.reps):
+    res = {w: {n: [] for n in names} for w in work}
+    for w, (fn, _) in work.items():
         for n in names:
-            res[n].append(timed(n))
-    algo = nblk * 4100
-    print(json.dumps({"gib": args.gib, "reps": args.reps, "identical_results": same,
-                      "results": {n: {"GB/s_median": round(algo / statistics.median(v) / 1e9, 1),
-                                      "GB/s_best": round(algo / min(v) / 1e9, 1),
-                                      "ms_median": round(statistics.median(v) * 1e3, 3)}
-                                  for n, v in res.items()}}, indent=1))
+            timed(fn, n)
+    for _ in range(args.reps):
+        for w, (fn, _) in work.items():
+            for n in names:
+                res[w][n].append(timed(fn, n))
+    print(json.dumps({"gib": args.gib, "reps": args.reps,
+                      "results": {w: {n: {"GB/s_median": round(work[w][1] / statistics.median(v) / 1e9, 1),
+                                          "ms_median": round(statistics.median(v) * 1e3, 3)}
+                                      for n, v in r.items()} for w, r in res.items()}}, indent=1))
 
 
 def main():
