@@ -85,8 +85,10 @@ def build(force: bool = False, asm: bool = False, verbose: bool = False, defines
             if verbose:
                 print(" ".join(cmd))
         list(ex.map(_run, jobs))
-    if force or jobs or _stale(lib_out, objs):
-        _run([hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", lib_out, *objs])
+    exports = os.path.join(CSRC, "exports.map")
+    if force or jobs or _stale(lib_out, objs + [exports]):
+        _run([hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", f"-Wl,--version-script={exports}",
+              "-o", lib_out, *objs])
     if asm:
         asmdir = os.path.join(ROOT, "build", "asm")
         os.makedirs(asmdir, exist_ok=True)

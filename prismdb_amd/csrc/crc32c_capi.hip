@@ -162,86 +162,92 @@ int GetCtx(DeviceCtx** out) {
   return 0;
 }
 
-// ---- split-path workspace, per (thread, device, stream) ----
+// ---- generic-path workspace, per (thread, device, stream) ----
+// Fixed part: split-path counters, segment records/results, long-span list.
+// Growing part: one 16-byte record per span of the largest batch seen (the
+// first call with a larger batch synchronises the stream and reallocates).
 struct Workspace {
   void* mem = nullptr;
+  prismdb::dev::SpanRec* rec = nullptr;
+  size_t cap_rec = 0;
   SplitWs ws{};
 };
 
 constexpr uint64_t kCapSeg = 1u << 20;   // 1 Mi segments = 32 GiB of long spans per call
 constexpr uint32_t kCapLong = 1u << 18;
 
-int GetWorkspace(hipStream_t s, SplitWs* out) {
+int GetWorkspace(hipStream_t s, size_t nspans, SplitWs* out) {
   thread_local std::map<std::pair<int, hipStream_t>, Workspace> cache;
   int device = 0;
   hipGetDevice(&device);
   Workspace& w = cache[{device, s}];
   if (w.mem == nullptr) {
-    const size_t bytes = 256 + kCapSeg * (8 + 4 + 4 + 4) + (size_t)kCapLong * (8 + 8 + 4);
+    const size_t bytes = 256 + kCapSeg * (16 + 4) + (size_t)kCapLong * (8 + 8 + 4);
     hipError_t e = hipMalloc(&w.mem, bytes);
     if (e != hipSuccess) {
       w.mem = nullptr;
-      return FailHip(e, "split workspace hipMalloc");
+      return FailHip(e, "workspace hipMalloc");
     }
     char* p = static_cast<char*>(w.mem);
     w.ws.counters = reinterpret_cast<SplitCounters*>(p);
     p += 256;
-    w.ws.seg_off = reinterpret_cast<uint64_t*>(p);
-    p += kCapSeg * 8;
+    w.ws.seg_rec = reinterpret_cast<prismdb::dev::SpanRec*>(p);
+    p += kCapSeg * 16;
     w.ws.long_span = reinterpret_cast<uint64_t*>(p);
     p += (size_t)kCapLong * 8;
     w.ws.long_first = reinterpret_cast<uint64_t*>(p);
     p += (size_t)kCapLong * 8;
-    w.ws.seg_len = reinterpret_cast<uint32_t*>(p);
-    p += kCapSeg * 4;
-    w.ws.seg_init = reinterpret_cast<uint32_t*>(p);
-    p += kCapSeg * 4;
     w.ws.seg_out = reinterpret_cast<uint32_t*>(p);
     p += kCapSeg * 4;
     w.ws.long_nseg = reinterpret_cast<uint32_t*>(p);
     w.ws.cap_seg = kCapSeg;
     w.ws.cap_long = kCapLong;
   }
+  if (w.cap_rec < nspans) {
+    if (w.rec != nullptr) {
+      hipStreamSynchronize(s);  // earlier batches on this stream may still read it
+      hipFree(w.rec);
+      w.rec = nullptr;
+      w.cap_rec = 0;
+    }
+    const size_t cap = nspans < 4096 ? 4096 : nspans + nspans / 4;
+    hipError_t e = hipMalloc(reinterpret_cast<void**>(&w.rec), cap * 16);
+    if (e != hipSuccess) return FailHip(e, "span record workspace hipMalloc");
+    w.cap_rec = cap;
+  }
+  w.ws.rec = w.rec;
   *out = w.ws;
   return 0;
 }
 
-// Launch sequence.  Spans that may exceed kLongSpan go through
-// plan -> span pass (long spans skipped) -> segment pass -> combine.
+// Launch sequence.  Fast path: one kernel.  Generic path:
+// plan (span records, long spans cut into segments) -> span pass (long spans
+// skipped) -> segment pass -> combine.
 int RunBatch(DeviceCtx& ctx, const SpanBatch& base_args, bool desc, bool verify, hipStream_t s) {
   SpanBatch a = base_args;
   a.tabs = ctx.tabs;
   a.role = prismdb::dev::kRoleSpans;
-  const bool may_be_long = desc || a.len_c > prismdb::dev::kLongSpan;
   // Fast path: fixed stride, 4-byte aligned, 4..4096-byte multiple-of-4 spans.
-  if (!desc && !verify && a.out != nullptr && (a.flags & prismdb::dev::kFlagWriteTrailer) == 0 && a.len_c >= 4 && a.len_c <= 4u * prismdb::dev::kChunkWords &&
-      (a.len_c & 3u) == 0 && (a.stride & 3u) == 0 && (reinterpret_cast<uintptr_t>(a.base) & 3u) == 0 &&
-      !g_force_generic) {
+  if (!desc && !verify && a.out != nullptr && (a.flags & prismdb::dev::kFlagWriteTrailer) == 0 &&
+      a.len_c >= 4 && a.len_c <= 4u * prismdb::dev::kChunkWords && (a.len_c & 3u) == 0 &&
+      (a.stride & 3u) == 0 && (reinterpret_cast<uintptr_t>(a.base) & 3u) == 0 && !g_force_generic) {
     hipError_t e = prismdb::dev::launch_fixed(a, ctx.cus, s);
     return e == hipSuccess ? 0 : FailHip(e, "fixed kernel launch");
   }
-  if (!may_be_long) {
-    a.skip_above = 0xFFFFFFFFu;
-    a.overflow = nullptr;
-    hipError_t e = prismdb::dev::launch_span(a, desc, verify, ctx.cus, s);
-    return e == hipSuccess ? 0 : FailHip(e, "span kernel launch");
-  }
   SplitWs ws{};
-  int rc = GetWorkspace(s, &ws);
+  int rc = GetWorkspace(s, a.n, &ws);
   if (rc != 0) return rc;
   hipError_t e = hipMemsetAsync(ws.counters, 0, sizeof(SplitCounters), s);
   if (e != hipSuccess) return FailHip(e, "hipMemsetAsync");
   a.skip_above = prismdb::dev::kLongSpan;
   a.overflow = &ws.counters->overflow;
+  a.rec = ws.rec;
   e = prismdb::dev::launch_plan(a, desc, ws, s);
   if (e != hipSuccess) return FailHip(e, "plan kernel launch");
-  e = prismdb::dev::launch_span(a, desc, verify, ctx.cus, s);
+  e = prismdb::dev::launch_span(a, verify, ctx.cus, s);
   if (e != hipSuccess) return FailHip(e, "span kernel launch");
   SpanBatch seg{};
   seg.base = a.base;
-  seg.off = ws.seg_off;
-  seg.len = ws.seg_len;
-  seg.init = ws.seg_init;
   seg.n = ws.cap_seg;
   seg.n_dev = &ws.counters->nseg;
   seg.out = ws.seg_out;
@@ -249,7 +255,8 @@ int RunBatch(DeviceCtx& ctx, const SpanBatch& base_args, bool desc, bool verify,
   seg.overflow = &ws.counters->overflow;
   seg.role = prismdb::dev::kRoleSegments;
   seg.tabs = ctx.tabs;
-  e = prismdb::dev::launch_span(seg, true, false, ctx.cus, s);
+  seg.rec = ws.seg_rec;
+  e = prismdb::dev::launch_span(seg, false, ctx.cus, s);
   if (e != hipSuccess) return FailHip(e, "segment kernel launch");
   e = prismdb::dev::launch_combine(a, desc, verify, ws, s);
   return e == hipSuccess ? 0 : FailHip(e, "combine kernel launch");

@@ -36,6 +36,9 @@ struct DeviceTables {
 
 enum : uint32_t { kRoleSpans = 0, kRoleSegments = 1 };
 
+// 16-byte span record with all geometry precomputed (crc32c_kernels.hip).
+typedef uint32_t SpanRec __attribute__((ext_vector_type(4)));
+
 struct SpanBatch {
   const uint8_t* base;
   const uint64_t* off;   // descriptor mode
@@ -53,6 +56,7 @@ struct SpanBatch {
   const uint32_t* overflow;         // nullable: split-path overflow flag
   uint32_t role;
   const DeviceTables* tabs;
+  const SpanRec* rec;               // span records (generic kernel)
 };
 
 struct SplitCounters {
@@ -63,9 +67,8 @@ struct SplitCounters {
 
 struct SplitWs {
   SplitCounters* counters;
-  uint64_t* seg_off;
-  uint32_t* seg_len;
-  uint32_t* seg_init;
+  SpanRec* rec;      // one per span of the batch
+  SpanRec* seg_rec;  // one per segment
   uint32_t* seg_out;
   uint64_t* long_span;
   uint64_t* long_first;
@@ -74,7 +77,7 @@ struct SplitWs {
   uint32_t cap_long;
 };
 
-hipError_t launch_span(const SpanBatch& a, bool desc, bool verify, int grid, hipStream_t s);
+hipError_t launch_span(const SpanBatch& a, bool verify, int grid, hipStream_t s);
 hipError_t launch_fixed(const SpanBatch& a, int grid, hipStream_t s);
 hipError_t launch_plan(const SpanBatch& a, bool desc, const SplitWs& ws, hipStream_t s);
 hipError_t launch_combine(const SpanBatch& a, bool desc, bool verify, const SplitWs& ws,

@@ -2,38 +2,39 @@
 //
 // What is computed: for every span i, crc32c::Extend(init_i, base+off_i, len_i)
 // (util/crc32c.cc:276-377), optionally Mask()ed (util/crc32c.h:27-31, as
-// TableBuilder::WriteRawBlock stores it, table/table_builder.cc:194-196) and/or
-// compared against the stored trailer (ReadBlock verify, table/format.cc:93-95).
+// TableBuilder::WriteRawBlock stores it, table/table_builder.cc:194-196),
+// optionally written back as the block trailer, and/or compared against the
+// stored trailer (ReadBlock verify, table/format.cc:93-95).
 //
-// How (one span per 64-lane wavefront, HBM-bound design):
-//   * The span is cut into head bytes (to 4-B alignment), W body words and
-//     tail bytes.  Body word i goes to lane (i - W) mod 64: the wave reads 256
-//     contiguous bytes per round (coalesced dword loads), rounds right-aligned
-//     so that every lane's last word is in the final round.
+// How (HBM-bound byte reduction; no MFMA):
+//   * A span is cut into head bytes (to 4-B alignment), W body words and tail
+//     bytes.  Body word i goes to lane (i - W) mod 64: the wave reads 256
+//     contiguous bytes per round, rounds right-aligned so that every lane's
+//     last word falls in the final round.
 //   * Each lane runs its own CRC stream with stride 256 B:
 //         acc <- shift_256(acc) ^ word
-//     where shift_256 (register advanced over 256 zero bytes) is four lookups
-//     in LDS stride tables.  The tables are replicated 32x, interleaved so
-//     that lane l always reads bank (l mod 32): ds_read_b32 never conflicts.
-//   * Lane l's stream ends 256-4l bytes before the body end, so its partial is
-//     moved there by a per-lane 32x32 GF(2) matrix held in 32 VGPRs
-//     (shift_{256-4l}), then the wave XOR-reduces with DPP.  The span's initial
-//     register (init, head bytes) is injected into body word 0.
-//   * Persistent grid (one 1024-thread workgroup per CU: the 128 KiB of LDS
-//     tables are loaded once per CU), spans dealt round-robin to waves, next
-//     chunk's loads issued before the current chunk is folded (register double
-//     buffer), descriptors staged 64 spans at a time in lanes.
-//   * Spans longer than kLongSpan are cut into kSegment pieces by a planner
-//     kernel, processed as independent spans, then stitched with the constant
-//     operator shift_kSegment (CRC combination) by a combine kernel.
+//     shift_256 = four lookups in LDS stride tables replicated 32x so that
+//     lane l always reads bank l mod 32 (ds_read_b32 never conflicts); each
+//     lookup address is one v_perm_b32.
+//   * Lane l's stream ends 256-4l bytes before the body end: eight lookups in
+//     lane l's nibble tables apply shift_{256-4l}, then the wave XOR-reduces
+//     with DPP.  The initial register (init, head bytes) enters with body word 0.
+//   * Persistent grid: one 1024-thread workgroup per CU (the 160 KiB of LDS
+//     tables are loaded once per CU), spans dealt round-robin to waves, two
+//     spans folded per wave at a time (two independent LDS chains), loads
+//     issued with inline asm one pair ahead and retired by counted vmcnt.
+//
+// Kernels:
+//   crc32c_fixed_kernel<K>  fixed stride, 4-B aligned, len <= 4 KiB (config 2)
+//   crc32c_plan_kernel      one thread per span: 16-byte span records (all
+//                           geometry precomputed), long spans cut into segments
+//   crc32c_span_kernel      everything else, driven by the span records
+//   crc32c_combine_kernel   stitches segments back into long spans
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "crc32c_device.h"
 
-#ifndef PRISMDB_SPAN_V1
-#define PRISMDB_SPAN_V1 0  // 1: previous generic kernel (compiler-managed loads), for A/B runs
-#endif
 #ifndef PRISMDB_RING
 #define PRISMDB_RING 4  // span buffers in the fixed kernel's prefetch ring (even)
 #endif
@@ -84,34 +85,6 @@ __device__ __forceinline__ uint32_t unmask_crc(uint32_t m) {
   return (r << 15) | (r >> 17);
 }
 
-// Wave-uniform description of one span.
-struct Geo {
-  const uint8_t* p;  // first byte
-  uint32_t len, init;
-  uint32_t h;        // head bytes (to 4-byte alignment), 0..3
-  uint32_t W;        // body words
-  uint32_t t;        // tail bytes, 0..3
-  uint32_t nch;      // chunks of kChunkWords body words (>= 1)
-  uint32_t pad;      // nch*kChunkWords - W: leading zero words of chunk 0
-  bool skip;         // handled by the long-span path instead
-};
-
-__device__ __forceinline__ Geo make_geo(const uint8_t* p, uint32_t len, uint32_t init, bool skip) {
-  Geo g;
-  g.p = p;
-  g.len = len;
-  g.init = init;
-  uint32_t h = (4u - ((uint32_t)(uintptr_t)p & 3u)) & 3u;
-  if (h > len) h = len;
-  g.h = h;
-  g.W = (len - h) >> 2;
-  g.t = (len - h) & 3u;
-  g.nch = g.W ? (g.W + kChunkWords - 1u) / kChunkWords : 1u;
-  g.pad = g.nch * kChunkWords - g.W;
-  g.skip = skip;
-  return g;
-}
-
 // LDS image of the stride tables (128 KiB): table k, entry e, copy c = lane%32
 // sits at byte ((k>>1) << 16) | (e << 8) | ((k&1) << 7) | (c << 2), so every
 // lookup address is one v_perm_b32: byte 1 <- byte k of acc, bytes 0 and 2
@@ -153,14 +126,6 @@ __device__ __forceinline__ uint32_t step256(const uint32_t* lds, const StrideLan
   return x ^ a2 ^ a3;
 }
 
-__device__ __forceinline__ uint32_t load_word(const uint8_t* p) {
-#if PRISMDB_NT_LOADS
-  return __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(p));
-#else
-  return *reinterpret_cast<const uint32_t*>(p);
-#endif
-}
-
 // shift_{256-4l}(acc) for this lane: eight nibble lookups in lane l's own
 // tables (entry [n][v] at word 64*(16n+v)+l, so bank = l mod 32).
 __device__ __forceinline__ uint32_t realign(const uint32_t* __restrict__ nibtab, uint32_t acc) {
@@ -170,229 +135,7 @@ __device__ __forceinline__ uint32_t realign(const uint32_t* __restrict__ nibtab,
   return v;
 }
 
-// Issue the body loads of chunk c of g into w[] (no wait).
-__device__ __forceinline__ void issue_chunk(const Geo& g, uint32_t c, uint32_t lane,
-                                            uint32_t (&w)[kRounds]) {
-  const uint8_t* body = g.p + g.h;
-  const int32_t i0 = (int32_t)(c * kChunkWords + lane) - (int32_t)g.pad;
-  if (c == 0 && g.pad != 0) {
-#pragma unroll
-    for (int j = 0; j < kRounds; ++j) {
-      const int32_t i = i0 + 64 * j;
-      const uint32_t byte_off = (uint32_t)(i < 0 ? 0 : i) * 4u;
-      w[j] = load_word(body + byte_off);
-    }
-  } else {
-    const uint32_t byte_off = (uint32_t)i0 * 4u;
-#pragma unroll
-    for (int j = 0; j < kRounds; ++j) w[j] = load_word(body + byte_off + 256u * j);
-  }
-}
-
-// Issue the edge-byte load of chunk c of a span into the chunk's own slot:
-// lanes 0..h-1 head bytes (first chunk), 3..3+t-1 tail bytes and 6..9 the
-// stored trailer (verify) (last chunk).
-template <bool kVerify>
-__device__ __forceinline__ uint32_t issue_edges(const Geo& g, uint32_t c, uint32_t lane) {
-  const uint8_t* src = nullptr;
-  const bool first = c == 0, last = c + 1 == g.nch;
-  if (first && lane < g.h)
-    src = g.p + lane;
-  else if (last && lane >= 3u && lane < 3u + g.t)
-    src = g.p + g.h + 4ull * g.W + (lane - 3u);
-  else if (kVerify && last && lane >= 6u && lane < 10u)
-    src = g.p + g.len + (lane - 6u);
-  uint32_t e = 0;
-  if (src != nullptr) e = *src;
-  return e;
-}
-
-struct Desc {
-  uint32_t off_lo, off_hi, len, init;
-};
-
 }  // namespace
-
-// ---------------------------------------------------------------------------
-// Main span kernel.
-// ---------------------------------------------------------------------------
-template <bool kDesc, bool kVerify>
-__global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
-  uint64_t n = a.n;
-  if (a.n_dev != nullptr) {
-    const uint64_t m = *a.n_dev;
-    n = m < n ? m : n;
-  }
-  uint32_t skip_above = a.skip_above;
-  if (a.overflow != nullptr && *a.overflow != 0u) {
-    if (a.role == kRoleSegments) n = 0;   // split path abandoned: nothing to do
-    else skip_above = 0xFFFFFFFFu;        // ...and the span pass takes every span whole
-  }
-  if (n == 0) return;
-
-  __shared__ uint32_t lds[kLdsWords];
-  const uint32_t tid = threadIdx.x;
-  load_tables(lds, a.tabs, tid);
-  const uint32_t lane = tid & 63u;
-  __syncthreads();
-
-  const StrideLanes tab = stride_lanes(lane);
-  const uint32_t* nibtab = lds + kTabWords + lane;
-  const uint64_t wave = rfl(blockIdx.x * kWavesPerGroup + (tid >> 6));
-  const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerGroup;
-  if (wave >= n) return;
-
-  // --- descriptor staging (variable batches): lane q holds span k = 64*G + q ---
-  Desc dcur{0, 0, 0, 0}, dnx{0, 0, 0, 0};
-  auto load_desc = [&](uint64_t group) -> Desc {
-    Desc d{0, 0, 0, 0};
-    const uint64_t b = wave + (group * 64u + lane) * nwaves;
-    if (b < n) {
-      const uint64_t o = a.off[b];
-      d.off_lo = (uint32_t)o;
-      d.off_hi = (uint32_t)(o >> 32);
-      d.len = a.len[b];
-      d.init = a.init != nullptr ? a.init[b] : 0u;
-    }
-    return d;
-  };
-  auto geo_of = [&](uint64_t k) -> Geo {
-    const uint64_t b = wave + k * nwaves;
-    uint64_t off;
-    uint32_t len, init;
-    if (kDesc) {
-      const uint32_t q = (uint32_t)(k & 63u);
-      off = ((uint64_t)readlane(dcur.off_hi, q) << 32) | readlane(dcur.off_lo, q);
-      len = readlane(dcur.len, q);
-      init = readlane(dcur.init, q);
-    } else {
-      off = b * a.stride;
-      len = a.len_c;
-      init = a.init_c;
-    }
-    return make_geo(a.base + off, len, init, len > skip_above);
-  };
-  if (kDesc) {
-    dcur = load_desc(0);
-    dnx = load_desc(1);
-  }
-
-  // --- task ring: task = (span ordinal k, chunk c); loads run kPrefetch tasks ahead ---
-  struct Task {
-    uint64_t k;
-    uint32_t c;
-    bool valid;
-    Geo g;
-  };
-  auto first_task = [&]() -> Task {
-    Task t;
-    t.k = 0;
-    t.c = 0;
-    t.valid = true;
-    t.g = geo_of(0);
-    return t;
-  };
-  auto next_task = [&](const Task& t) -> Task {
-    Task u = t;
-    u.c = t.c + 1;
-    if (u.c == t.g.nch) {
-      u.k = t.k + 1;
-      u.c = 0;
-      u.valid = t.valid && wave + u.k * nwaves < n;
-      if (u.valid) {
-        if (kDesc && (u.k & 63u) == 0) {
-          dcur = dnx;
-          dnx = load_desc((u.k >> 6) + 1);
-        }
-        u.g = geo_of(u.k);
-      }
-    }
-    return u;
-  };
-  auto issue = [&](const Task& t, uint32_t (&w)[kRounds], uint32_t& e) {
-    if (t.valid && !t.g.skip) {
-      if (t.g.W) issue_chunk(t.g, t.c, lane, w);
-      if ((t.c == 0 && t.g.h) || (t.c + 1 == t.g.nch && (t.g.t | (uint32_t)kVerify)))
-        e = issue_edges<kVerify>(t.g, t.c, lane);
-    }
-  };
-
-  // Three chunk buffers in a ring, the loop unrolled three times so every
-  // buffer keeps a static register name (a register copy between ring slots
-  // would force a vmcnt(0) on the freshest loads and undo the prefetch).
-  Task t0 = first_task();
-  Task t1 = next_task(t0);
-  uint32_t bA[kRounds], bB[kRounds], bC[kRounds];
-#pragma unroll
-  for (int j = 0; j < kRounds; ++j) bA[j] = bB[j] = bC[j] = 0u;
-  uint32_t eA = 0, eB = 0, eC = 0;
-  issue(t0, bA, eA);
-  issue(t1, bB, eB);
-
-  uint32_t r = 0, acc = 0;
-  // Fold t0 (data in `cur`, edge bytes in `ecur`), first issuing t0+2 into `nxt`.
-  auto step = [&](uint32_t (&cur)[kRounds], uint32_t ecur, uint32_t (&nxt)[kRounds],
-                  uint32_t& enxt) -> bool {
-    const Task t2 = next_task(t1);
-    issue(t2, nxt, enxt);  // two tasks ahead of the one folded below
-
-    const Geo& g = t0.g;
-    const uint32_t c = t0.c;
-    if (!g.skip) {
-      // -- span start: initial register through the head bytes --
-      if (c == 0) {
-        r = g.init ^ kConditioning;
-        for (uint32_t q = 0; q < g.h; ++q) r = feed_byte(r, readlane(ecur, q));
-        acc = 0;
-      }
-      // -- fold this chunk --
-      if (g.W) {
-        if (c == 0) {
-          const uint32_t jstart = g.pad >> 6;
-          const uint32_t l0 = g.pad & 63u;
-#pragma unroll
-          for (int j = 0; j < kRounds; ++j) {
-            if ((uint32_t)j < jstart) continue;
-            uint32_t w = cur[j];
-            if ((uint32_t)j == jstart) {
-              w = lane >= l0 ? w : 0u;
-              w ^= lane == l0 ? r : 0u;  // initial register enters with body word 0
-            }
-            acc = step256(lds, tab, acc, w);
-          }
-        } else {
-#pragma unroll
-          for (int j = 0; j < kRounds; ++j) acc = step256(lds, tab, acc, cur[j]);
-        }
-      }
-      // -- span end: per-lane realignment, wave reduction, tail, output --
-      if (c + 1 == g.nch) {
-        if (g.W) {
-          r = wave_xor(realign(nibtab, acc));
-        }
-        for (uint32_t q = 0; q < g.t; ++q) r = feed_byte(r, readlane(ecur, 3u + q));
-        const uint32_t crc = r ^ kConditioning;
-        const uint64_t b = wave + t0.k * nwaves;
-        if (lane == 0) {
-          const uint32_t res = (a.flags & kFlagMask) ? mask_crc(crc) : crc;
-          if (a.out != nullptr) a.out[b] = res;
-          if (a.flags & kFlagWriteTrailer) store_le32(g.p + g.len, res);
-          if (kVerify && a.mismatch != nullptr) {
-            const uint32_t stored = readlane(ecur, 6) | (readlane(ecur, 7) << 8) |
-                                    (readlane(ecur, 8) << 16) | (readlane(ecur, 9) << 24);
-            a.mismatch[b] = crc != unmask_crc(stored) ? 1 : 0;
-          }
-        }
-      }
-    }
-    if (!t1.valid) return false;
-    t0 = t1;
-    t1 = t2;
-    return true;
-  };
-  while (step(bA, eA, bC, eC) && step(bB, eB, bA, eA) && step(bC, eC, bB, eB)) {
-  }
-}
 
 // Inline-asm dword load, non-temporal, SGPR base + 32-bit VGPR byte offset.
 // The compiler does not track these: consumers must go through wait_ring.
@@ -443,16 +186,6 @@ __device__ __forceinline__ void wait_ring(uint32_t (&w)[kRounds]) {
                : "memory");
 }
 
-// ---------------------------------------------------------------------------
-// Generic span kernel, v2: two independent span streams per wave folded in
-// lockstep (stream 0 takes the wave's even span ordinals, stream 1 the odd
-// ones), every load an inline-asm BUFFER load issued two tasks ahead and
-// retired by a counted vmcnt.  A task is one 4 KiB chunk of one span and
-// always issues exactly 17 loads (16 body dwords + 1 edge byte): loads outside
-// the span hit the buffer range check and return 0 without touching memory,
-// which provides the right-aligned zero padding of chunk 0 and lets invalid or
-// skipped tasks run through the same code.
-// ---------------------------------------------------------------------------
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 // Uniform-address load through the scalar cache (constant address space).
@@ -504,36 +237,68 @@ __device__ __forceinline__ void wait_task(uint32_t (&w)[kRounds], uint32_t& e) {
 
 // Wave-uniform task (span ordinal q, chunk c); the span's geometry is
 // recomputed from (p, len) when needed to keep the SGPR footprint small.
+// ---------------------------------------------------------------------------
+// Span records (written by crc32c_plan_kernel, one thread per span):
+//   x = body address bits 0-31          body = first 4-B aligned byte of the span
+//   y = body bits 32-47 | pad << 16 | h << 26 | t << 28 | long << 30
+//   z = body bytes (4W)                 W body words, h head bytes, t tail bytes
+//   w = init
+// pad = nch*1024 - W leading zero words of chunk 0 (nch = ceil(W/1024) >= 1).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ SpanRec make_rec(const uint8_t* p, uint32_t len, uint32_t init, bool lng) {
+  uint32_t h = (4u - ((uint32_t)(uintptr_t)p & 3u)) & 3u;
+  if (h > len) h = len;
+  const uint32_t W = (len - h) >> 2, t = (len - h) & 3u;
+  const uint32_t nch = W ? (W + kChunkWords - 1u) / kChunkWords : 1u;
+  const uint32_t pad = (nch * kChunkWords - W) & 1023u;  // W == 0: every load is out of range anyway
+  const uint64_t body = reinterpret_cast<uint64_t>(p + h);
+  SpanRec r;
+  r.x = (uint32_t)body;
+  r.y = ((uint32_t)(body >> 32) & 0xffffu) | (pad << 16) | (h << 26) | (t << 28) | ((uint32_t)lng << 30);
+  r.z = 4u * W;
+  r.w = init;
+  return r;
+}
+
+// Wave-uniform task: chunk c of the span with record r at index b.
 struct Task {
-  const uint8_t* p;
-  uint64_t q;
-  uint32_t len, init;
+  uint64_t b;
+  SpanRec r;
   uint32_t c;
   bool valid, skip;
-  __device__ uint32_t h() const {
-    const uint32_t x = (4u - ((uint32_t)(uintptr_t)p & 3u)) & 3u;
-    return x < len ? x : len;
+  __device__ const uint8_t* body() const {
+    return reinterpret_cast<const uint8_t*>(((uint64_t)(r.y & 0xffffu) << 32) | r.x);
   }
-  __device__ uint32_t W() const { return (len - h()) >> 2; }
-  __device__ uint32_t t() const { return (len - h()) & 3u; }
-  __device__ uint32_t nch() const {
-    const uint32_t w = W();
-    return w ? (w + kChunkWords - 1u) / kChunkWords : 1u;
-  }
-  __device__ uint32_t pad() const { return nch() * kChunkWords - W(); }
+  __device__ uint32_t pad() const { return (r.y >> 16) & 1023u; }
+  __device__ uint32_t h() const { return (r.y >> 26) & 3u; }
+  __device__ uint32_t t() const { return (r.y >> 28) & 3u; }
+  __device__ bool lng() const { return (r.y >> 30) & 1u; }
+  __device__ uint32_t nch() const { return r.z ? (r.z + 4095u) >> 12 : 1u; }
+  __device__ uint32_t len() const { return h() + r.z + t(); }
+  __device__ const uint8_t* start() const { return body() - h(); }
 };
 
-template <bool kDesc, bool kVerify>
-__global__ __launch_bounds__(kThreads) void crc32c_span2_kernel(SpanBatch a) {
+// ---------------------------------------------------------------------------
+// Record-driven span kernel: two span streams per wave (stream s takes the
+// wave's spans b = wave + (2q + s) * nwaves) folded in lockstep, every load an
+// inline-asm BUFFER load issued one slot ahead and retired by a counted vmcnt.
+// A task is one 4 KiB chunk and always issues exactly 17 loads (16 body dwords
+// + 1 edge byte): loads outside the span hit the buffer range check and return
+// 0 without touching memory, which gives chunk 0 its right-aligned zero padding
+// and lets invalid or skipped tasks run through the same code.  Records come
+// through the scalar cache, one span ahead per stream.
+// ---------------------------------------------------------------------------
+template <bool kVerify>
+__global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
   uint64_t n = a.n;
   if (a.n_dev != nullptr) {
     const uint64_t m = *a.n_dev;
     n = m < n ? m : n;
   }
-  uint32_t skip_above = a.skip_above;
+  bool skip_long = a.role == kRoleSpans;  // long spans go through segments...
   if (a.overflow != nullptr && *a.overflow != 0u) {
-    if (a.role == kRoleSegments) n = 0;
-    else skip_above = 0xFFFFFFFFu;
+    if (a.role == kRoleSegments) n = 0;   // ...unless the segment workspace overflowed
+    skip_long = false;
   }
   if (n == 0) return;
 
@@ -547,45 +312,24 @@ __global__ __launch_bounds__(kThreads) void crc32c_span2_kernel(SpanBatch a) {
   const uint64_t wave = rfl(blockIdx.x * kWavesPerGroup + (tid >> 6));
   const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerGroup;
   if (wave >= n) return;
+  const uint64_t step = 2 * nwaves;
 
-  // span b of stream s, ordinal q: b = wave + (2q + s) * nwaves
-  auto span_of = [&](int s, uint64_t q) -> uint64_t { return wave + (2 * q + (uint64_t)s) * nwaves; };
-  // Descriptors come through the scalar cache (constant address space), one
-  // span ahead per stream: a vector load here would make the compiler wait
-  // vmcnt(0) and drain the asm load ring.
-  struct Desc {
-    uint64_t off;
-    uint32_t len, init;
+  auto read_rec = [&](uint64_t b) -> SpanRec {
+    SpanRec r{0u, 0u, 0u, 0u};
+    if (b < n) r = const_load(a.rec, b);
+    return r;
   };
-  auto read_desc = [&](int s, uint64_t q) -> Desc {
-    Desc d{0, 0, 0};
-    const uint64_t b = span_of(s, q);
-    if (b < n) {
-      if (kDesc) {
-        d.off = const_load(a.off, b);
-        d.len = const_load(a.len, b);
-        d.init = a.init != nullptr ? const_load(a.init, b) : 0u;
-      } else {
-        d.off = b * a.stride;
-        d.len = a.len_c;
-        d.init = a.init_c;
-      }
-    }
-    return d;
-  };
-  auto make_task = [&](int s, uint64_t q, const Desc& d) -> Task {
+  auto make_task = [&](uint64_t b, const SpanRec& r) -> Task {
     Task t;
-    t.q = q;
+    t.b = b;
+    t.r = r;
     t.c = 0;
-    t.valid = span_of(s, q) < n;
-    t.p = a.base + d.off;
-    t.len = d.len;
-    t.init = d.init;
-    t.skip = !t.valid || d.len > skip_above;
+    t.valid = b < n;
+    t.skip = !t.valid || (skip_long && t.lng());
     return t;
   };
-  Desc pend[2];           // descriptor of the span after each stream's newest task
-  uint64_t newest[2] = {0, 0};
+  SpanRec pend[2];  // record of the span after each stream's newest task
+  uint64_t pend_b[2];
   bool refill[2] = {false, false};
   auto next_task = [&](int s, const Task& t) -> Task {
     if (t.c + 1 < t.nch()) {
@@ -593,31 +337,31 @@ __global__ __launch_bounds__(kThreads) void crc32c_span2_kernel(SpanBatch a) {
       u.c = t.c + 1;
       return u;
     }
-    Task u = make_task(s, t.q + 1, pend[s]);
+    Task u = make_task(pend_b[s], pend[s]);
     u.valid = u.valid && t.valid;
     u.skip = u.skip || !u.valid;
-    newest[s] = t.q + 1;
     refill[s] = true;
     return u;
   };
-  auto refill_desc = [&]() {  // after both streams took theirs: the scalar wait covers only older loads
+  auto refill_recs = [&]() {  // after both streams took theirs: the scalar wait covers only older loads
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       if (refill[s]) {
         refill[s] = false;
-        pend[s] = read_desc(s, newest[s] + 1);
+        pend_b[s] += step;
+        pend[s] = read_rec(pend_b[s]);
       }
     }
   };
   // 17 loads, always.
   auto issue = [&](const Task& t, uint32_t (&w)[kRounds], uint32_t& e) {
     const bool live = !t.skip;
-    const uint32_t h = t.h(), W = t.W(), tl = t.t(), nch = t.nch(), pad = nch * kChunkWords - W;
-    u32x4 rb = buffer_rsrc(t.p + h, live ? 4u * W : 0u);
-    u32x4 re = buffer_rsrc(t.p, live ? t.len + (kVerify ? 4u : 0u) : 0u);
-    // The descriptors were just written by v_readfirstlane (VALU -> SGPR) and
-    // the buffer loads below read them from inside asm, where hipcc inserts no
-    // wait states: 5 are required (cdna_hip_programming.md 5.7 item 2).
+    const uint32_t pad = t.pad(), h = t.h(), tl = t.t(), nch = t.nch(), len = t.len();
+    u32x4 rb = buffer_rsrc(t.body(), live ? t.r.z : 0u);
+    u32x4 re = buffer_rsrc(t.start(), live ? len + (kVerify ? 4u : 0u) : 0u);
+    // The descriptors may come from v_readfirstlane (VALU -> SGPR) and the
+    // buffer loads read them inside asm, where hipcc inserts no wait states:
+    // 5 are required (cdna_hip_programming.md 5.7 item 2).
     asm volatile("s_nop 4" : "+s"(rb), "+s"(re));
     const int32_t i0 = (int32_t)(t.c * kChunkWords + lane) - (int32_t)pad;
     if (t.c == 0 && pad != 0) {
@@ -635,8 +379,8 @@ __global__ __launch_bounds__(kThreads) void crc32c_span2_kernel(SpanBatch a) {
     const bool first = t.c == 0, last = t.c + 1 == nch;
     uint32_t eoff = 0xFFFFFFFFu;
     if (first && lane < h) eoff = lane;
-    if (last && lane >= 3u && lane < 3u + tl) eoff = h + 4u * W + (lane - 3u);
-    if (kVerify && last && lane >= 6u && lane < 10u) eoff = t.len + (lane - 6u);
+    if (last && lane >= 3u && lane < 3u + tl) eoff = h + t.r.z + (lane - 3u);
+    if (kVerify && last && lane >= 6u && lane < 10u) eoff = len + (lane - 6u);
     e = buf_ubyte(re, eoff);
   };
 
@@ -646,13 +390,13 @@ __global__ __launch_bounds__(kThreads) void crc32c_span2_kernel(SpanBatch a) {
   // Start of a chunk: head bytes and the initial-register injection (chunk 0).
   auto begin = [&](int s, const Task& t, uint32_t (&w)[kRounds], uint32_t e) {
     if (t.c == 0) {
-      const uint32_t h = t.h(), W = t.W();
-      uint32_t rr = t.init ^ kConditioning;
+      const uint32_t h = t.h();
+      uint32_t rr = t.r.w ^ kConditioning;
       for (uint32_t qb = 0; qb < h; ++qb) rr = feed_byte(rr, readlane(e, qb));
       r[s] = rr;
       acc[s] = 0u;
-      if (W) {
-        const uint32_t pad = t.nch() * kChunkWords - W;
+      if (t.r.z) {
+        const uint32_t pad = t.pad();
         const uint32_t inj = lane == (pad & 63u) ? rr : 0u;  // enters with body word 0
         switch (pad >> 6) {
 #define PRISMDB_INJ(J) \
@@ -671,19 +415,18 @@ __global__ __launch_bounds__(kThreads) void crc32c_span2_kernel(SpanBatch a) {
   };
   // End of a span: tail bytes, conditioning, outputs.
   auto finish = [&](int s, const Task& t, uint32_t e, uint32_t body) {
-    uint32_t rr = t.W() ? body : r[s];
+    uint32_t rr = t.r.z ? body : r[s];
     const uint32_t tl = t.t();
     for (uint32_t qb = 0; qb < tl; ++qb) rr = feed_byte(rr, readlane(e, 3u + qb));
     const uint32_t crc = rr ^ kConditioning;
-    const uint64_t b = span_of(s, t.q);
     if (lane == 0) {
       const uint32_t res = (a.flags & kFlagMask) ? mask_crc(crc) : crc;
-      if (a.out != nullptr) a.out[b] = res;
-      if (a.flags & kFlagWriteTrailer) store_le32(t.p + t.len, res);
+      if (a.out != nullptr) a.out[t.b] = res;
+      if (a.flags & kFlagWriteTrailer) store_le32(t.body() + t.r.z + tl, res);
       if (kVerify && a.mismatch != nullptr) {
         const uint32_t stored = readlane(e, 6) | (readlane(e, 7) << 8) | (readlane(e, 8) << 16) |
                                 (readlane(e, 9) << 24);
-        a.mismatch[b] = crc != unmask_crc(stored) ? 1 : 0;
+        a.mismatch[t.b] = crc != unmask_crc(stored) ? 1 : 0;
       }
     }
   };
@@ -714,19 +457,22 @@ __global__ __launch_bounds__(kThreads) void crc32c_span2_kernel(SpanBatch a) {
   };
 
   // Ring: two slots x two streams, compile-time slot indices (loop unrolled
-  // over the slots, as in the fixed kernel) so no buffer register is copied
-  // across the back-edge while its loads are in flight.  Fold slot `sl` while
-  // the other slot's two tasks are in flight, then refill slot `sl`.
+  // over the slots) so no buffer register is copied across the back-edge
+  // while its loads are in flight.  Fold slot `sl` while the other slot's two
+  // tasks are in flight, then refill slot `sl`.
   Task tk[2][2];
   uint32_t wb[2][2][kRounds];
   uint32_t eb[2][2];
-  tk[0][0] = make_task(0, 0, read_desc(0, 0));
-  tk[0][1] = make_task(1, 0, read_desc(1, 0));
-  pend[0] = read_desc(0, 1);
-  pend[1] = read_desc(1, 1);
+#pragma unroll
+  for (int st = 0; st < 2; ++st) {
+    const uint64_t b0 = wave + (uint64_t)st * nwaves;
+    tk[0][st] = make_task(b0, read_rec(b0));
+    pend_b[st] = b0 + step;
+    pend[st] = read_rec(pend_b[st]);
+  }
   tk[1][0] = next_task(0, tk[0][0]);
   tk[1][1] = next_task(1, tk[0][1]);
-  refill_desc();
+  refill_recs();
 #pragma unroll
   for (int sl = 0; sl < 2; ++sl) {
     issue(tk[sl][0], wb[sl][0], eb[sl][0]);
@@ -742,7 +488,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_span2_kernel(SpanBatch a) {
       if (!tk[sl ^ 1][0].valid && !tk[sl ^ 1][1].valid) goto drained;
       tk[sl][0] = next_task(0, tk[sl ^ 1][0]);
       tk[sl][1] = next_task(1, tk[sl ^ 1][1]);
-      refill_desc();
+      refill_recs();
       issue(tk[sl][0], wb[sl][0], eb[sl][0]);
       issue(tk[sl][1], wb[sl][1], eb[sl][1]);
     }
@@ -836,17 +582,24 @@ drained:
 }
 
 // ---------------------------------------------------------------------------
-// Long-span planner: spans longer than kLongSpan become segments
-// [first piece of len - (nseg-1)*kSegment bytes with the span's init]
-// followed by nseg-1 pieces of kSegment bytes with init 0xFFFFFFFF (raw).
+// Planner: one thread per span writes its record; spans longer than
+// skip_above become segments [first piece of len - (nseg-1)*kSegment bytes
+// with the span's init] + nseg-1 pieces of kSegment bytes with init
+// 0xFFFFFFFF (Extend(~0, d) ^ ~0 is the raw register R(0, d)), each with its
+// own record for the segment pass.
 // ---------------------------------------------------------------------------
 template <bool kDesc>
 __global__ __launch_bounds__(256) void crc32c_plan_kernel(SpanBatch a, SplitWs ws) {
   const uint64_t n = a.n;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t off = kDesc ? a.off[i] : i * a.stride;
     const uint32_t len = kDesc ? a.len[i] : a.len_c;
-    if (len <= a.skip_above) continue;
+    const uint32_t init = kDesc ? (a.init != nullptr ? a.init[i] : 0u) : a.init_c;
+    const uint8_t* p = a.base + off;
+    const bool lng = len > a.skip_above;
+    ws.rec[i] = make_rec(p, len, init, lng);
+    if (!lng) continue;
     const uint32_t nseg = (len + kSegment - 1u) / kSegment;
     const uint32_t first = len - (nseg - 1u) * kSegment;
     const uint64_t pos = atomicAdd((unsigned long long*)&ws.counters->nseg, (unsigned long long)nseg);
@@ -855,19 +608,12 @@ __global__ __launch_bounds__(256) void crc32c_plan_kernel(SpanBatch a, SplitWs w
       atomicOr(&ws.counters->overflow, 1u);
       continue;
     }
-    const uint64_t off = kDesc ? a.off[i] : i * a.stride;
-    const uint32_t init = kDesc ? (a.init != nullptr ? a.init[i] : 0u) : a.init_c;
     ws.long_span[li] = i;
     ws.long_first[li] = pos;
     ws.long_nseg[li] = nseg;
-    ws.seg_off[pos] = off;
-    ws.seg_len[pos] = first;
-    ws.seg_init[pos] = init;
-    for (uint32_t s = 1; s < nseg; ++s) {
-      ws.seg_off[pos + s] = off + first + (uint64_t)(s - 1u) * kSegment;
-      ws.seg_len[pos + s] = kSegment;
-      ws.seg_init[pos + s] = kConditioning;  // Extend(0xFFFFFFFF, d) ^ ~0 == raw register R(0, d)
-    }
+    ws.seg_rec[pos] = make_rec(p, first, init, false);
+    for (uint32_t s = 1; s < nseg; ++s)
+      ws.seg_rec[pos + s] = make_rec(p + first + (uint64_t)(s - 1u) * kSegment, kSegment, kConditioning, false);
   }
 }
 
@@ -905,22 +651,11 @@ __global__ __launch_bounds__(256) void crc32c_combine_kernel(SpanBatch a, SplitW
 }
 
 // ---------------------------------------------------------------------------
-// Host-side launchers (called from crc32c_capi.cc through crc32c_device.h).
+// Host-side launchers (called from crc32c_capi.hip through crc32c_device.h).
 // ---------------------------------------------------------------------------
-hipError_t launch_span(const SpanBatch& a, bool desc, bool verify, int grid, hipStream_t s) {
-#if PRISMDB_SPAN_V1
-#define PRISMDB_SPAN crc32c_span_kernel
-#else
-#define PRISMDB_SPAN crc32c_span2_kernel
-#endif
-  if (desc) {
-    if (verify) PRISMDB_SPAN<true, true><<<grid, kThreads, 0, s>>>(a);
-    else PRISMDB_SPAN<true, false><<<grid, kThreads, 0, s>>>(a);
-  } else {
-    if (verify) PRISMDB_SPAN<false, true><<<grid, kThreads, 0, s>>>(a);
-    else PRISMDB_SPAN<false, false><<<grid, kThreads, 0, s>>>(a);
-  }
-#undef PRISMDB_SPAN
+hipError_t launch_span(const SpanBatch& a, bool verify, int grid, hipStream_t s) {
+  if (verify) crc32c_span_kernel<true><<<grid, kThreads, 0, s>>>(a);
+  else crc32c_span_kernel<false><<<grid, kThreads, 0, s>>>(a);
   return hipGetLastError();
 }
 

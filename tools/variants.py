@@ -21,14 +21,17 @@ VDIR = os.path.join(ROOT, "tools", "_build", "variants")
 
 VARIANTS = {
     "base": {"PRISMDB_RING": 4, "PRISMDB_NT_LOADS": 1},
-    "span_v1": {"PRISMDB_SPAN_V1": 1},
 }
+# Libraries built elsewhere (e.g. from an older commit in a git worktree) and
+# dropped into VDIR as lib_<name>.so join the comparison with --only <name>.
 
 
 def do_build(names):
     from prismdb_amd.build import build
 
     for name in names:
+        if name not in VARIANTS:
+            continue
         print(build(defines=VARIANTS[name], lib_path=os.path.join(VDIR, f"lib_{name}.so")))
 
 
