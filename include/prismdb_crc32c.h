@@ -12,6 +12,8 @@
  *   leveldb_crc32c_batch*         N x crc32c::Value (+Extend type byte, +Mask) as issued by
  *                                 TableBuilder::WriteRawBlock      table/table_builder.cc:185-202
  *   ..._batch* with mismatch out  N x ReadBlock's verify          table/format.cc:91-102
+ *   ..._batch* with LOG_HEADER    N x log::Writer::EmitPhysicalRecord's crc / log::Reader's
+ *                                 check                           db/log_writer.cc:94-97, db/log_reader.cc:231-245
  *   leveldb_crc32c_accelerated    crc32c's CanAccelerateCRC32C    util/crc32c.cc:267-274
  *                                 (port::AcceleratedCRC32C hook   port/port_stdcxx.h:141-151)
  *
@@ -42,6 +44,14 @@ extern "C" {
  * TableBuilder::WriteRawBlock does (table/table_builder.cc:192-197).  The
  * buffer must be writable; not combinable with verify (mismatch != NULL). */
 #define PRISMDB_CRC32C_WRITE_TRAILER 0x2u
+/* log (WAL / MANIFEST) physical-record layout: the stored checksum that verify
+ * compares against, and that WRITE_TRAILER writes, is the 4 LE bytes 6 bytes
+ * BEFORE the span instead of right after it.  A log record is
+ * crc[4] | length[2] | type[1] | payload: pass span = type||payload, i.e.
+ * off = record + 6, len = 1 + length (db/log_writer.cc:94-97 computes
+ * Mask(Extend(type_crc[t], payload)) == Mask(Value(type||payload));
+ * db/log_reader.cc:231-245 checks Value(header + 6, 1 + length)). */
+#define PRISMDB_CRC32C_LOG_HEADER 0x4u
 
 /* error codes */
 #define PRISMDB_CRC32C_EINVAL (-1)  /* bad argument */
@@ -97,7 +107,9 @@ int leveldb_crc32c_batch(const void* dev_base, const uint64_t* dev_off, const ui
  * staging when host_base is pageable; directly when it is pinned/registered)
  * -> batch kernel -> results back, three chunks in flight on the engine's own
  * streams.  Synchronous; out/mismatch are host arrays (either may be NULL).
- * flags: PRISMDB_CRC32C_MASK only.  Uses the current HIP device.
+ * flags: PRISMDB_CRC32C_MASK, PRISMDB_CRC32C_LOG_HEADER (verify log records:
+ * the 6 header bytes before each span travel with it).  Uses the current HIP
+ * device.
  */
 int leveldb_crc32c_batch_host(const void* host_base, const uint64_t* off, const uint32_t* len,
                               const uint32_t* init, size_t n, uint32_t* out, uint8_t* mismatch,

@@ -14,6 +14,8 @@ by oracle/Makefile, see ref_shim.cc) and writes data-only fixtures:
   tests/golden/crc32c_vectors.json  [off, len, init, Extend(init, input[off:off+len]), Mask(.)]
   tests/golden/stream_vectors.json  long spans over the regenerable splitmix64 stream
   tests/golden/sst_small.ldb/.json  SST written and re-verified by the reference TableBuilder
+  tests/golden/log_cases.bin/.json  log files written by the reference log::Writer (db/log_test.cc
+                                    scenarios + seeded damage) and what log::Reader returns for them
 
 The fixtures hold reference OUTPUTS only; no reference source travels with them.
 """
@@ -134,6 +136,9 @@ def main() -> int:
     # --- reference-built SST ---
     subprocess.check_call([os.path.join(HERE, "_ref", "sst_fixture"), os.path.join(GOLD, "sst_small.ldb"),
                            os.path.join(GOLD, "sst_small.json"), "64", "980", "4096"])
+    # --- reference-written / reference-read log files ---
+    subprocess.check_call([os.path.join(HERE, "_ref", "log_fixture"), os.path.join(GOLD, "log_cases")],
+                          stderr=subprocess.DEVNULL)  # the reference reader traces every block read to stderr
     print(f"wrote {len(kat['vectors'])} KATs, {len(rows)} sweep vectors, {len(srows)} stream vectors")
     return 0
 

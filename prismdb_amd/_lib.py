@@ -29,6 +29,9 @@ C_ABI_SYMBOLS = (
     "prismdb_fill_synthetic",
     "leveldb_sst_block_spans",
     "leveldb_sst_last_error",
+    "leveldb_log_scan",
+    "leveldb_log_replay",
+    "leveldb_log_reason",
 )
 # The C++ surface (util/crc32c.h): crc32c::Extend(uint32_t, const char*, size_t).
 CXX_EXTEND_SYMBOL = "_ZN7leveldb6crc32c6ExtendEjPKcm"

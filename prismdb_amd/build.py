@@ -26,7 +26,7 @@ LIB = os.path.join(LIBDIR, "libprismdb_crc32c.so")
 
 ARCH = os.environ.get("PRISMDB_OFFLOAD_ARCH", "gfx950")
 HIP_SOURCES = ["crc32c_kernels.hip", "crc32c_capi.hip", "crc32c_pipeline.hip", "synth.hip"]
-CXX_SOURCES = ["crc32c_host.cc", "sst.cc"]
+CXX_SOURCES = ["crc32c_host.cc", "sst.cc", "log_reader.cc"]
 HEADERS = ["crc32c_device.h", "crc32c_gf2.h"]
 
 
@@ -64,6 +64,7 @@ def build(force: bool = False, asm: bool = False, verbose: bool = False, defines
         os.path.join(ROOT, "include", "prismdb_crc32c.h"),
         os.path.join(ROOT, "include", "prismdb_synth.h"),
         os.path.join(ROOT, "include", "prismdb_sst.h"),
+        os.path.join(ROOT, "include", "prismdb_log.h"),
         os.path.join(ROOT, "include", "util", "crc32c.h"),
     ]
     common = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function"]

@@ -27,6 +27,7 @@ from ._lib import check, lib
 kMaskDelta = 0xA282EAD8
 FLAG_MASK = 0x1
 FLAG_WRITE_TRAILER = 0x2
+FLAG_LOG_HEADER = 0x4
 
 
 def _bytes(data) -> bytes:
@@ -110,7 +111,8 @@ def batch_fixed(buf, stride: int, length: int, nblocks: int, init: int = 0, *, m
 
 
 def batch(buf, off, lens, init=None, *, mask: bool = False, verify: bool = False, out=None,
-          mismatch=None, stream=None, trailer: bool = False) -> Tuple[object, Optional[object]]:
+          mismatch=None, stream=None, trailer: bool = False,
+          log_header: bool = False) -> Tuple[object, Optional[object]]:
     """CRC32C of arbitrary spans buf[off[i] : off[i]+lens[i]] (int64 off, int32 lens, int32 init).
 
     trailer=True also stores each (masked, with mask=True) result as 4 LE bytes
@@ -133,12 +135,13 @@ def batch(buf, off, lens, init=None, *, mask: bool = False, verify: bool = False
     rc = lib().leveldb_crc32c_batch(
         buf.data_ptr(), off.data_ptr(), lens.data_ptr(), init.data_ptr() if init is not None else None, n,
         out.data_ptr(), mismatch.data_ptr() if verify else None,
-        (FLAG_MASK if mask else 0) | (FLAG_WRITE_TRAILER if trailer else 0), _stream_ptr(stream))
+        (FLAG_MASK if mask else 0) | (FLAG_WRITE_TRAILER if trailer else 0) | (FLAG_LOG_HEADER if log_header else 0),
+        _stream_ptr(stream))
     check(rc, "leveldb_crc32c_batch")
     return out, (mismatch if verify else None)
 
 
-def batch_host(base, off, lens, init=None, *, mask: bool = False, verify: bool = False):
+def batch_host(base, off, lens, init=None, *, mask: bool = False, verify: bool = False, log_header: bool = False):
     """Host-resident batch: numpy (or pinned torch CPU tensor) buffer and
     descriptors in host memory; streamed through the device by the engine.
     Returns (crc uint32[n], mismatch uint8[n] or None) as numpy arrays."""
@@ -153,7 +156,8 @@ def batch_host(base, off, lens, init=None, *, mask: bool = False, verify: bool =
     ptr = base.data_ptr() if hasattr(base, "data_ptr") else base.ctypes.data
     rc = lib().leveldb_crc32c_batch_host(ptr, off.ctypes.data, lens.ctypes.data,
                                          ini.ctypes.data if ini is not None else None, n, out.ctypes.data,
-                                         mm.ctypes.data if verify else None, FLAG_MASK if mask else 0)
+                                         mm.ctypes.data if verify else None,
+                                         (FLAG_MASK if mask else 0) | (FLAG_LOG_HEADER if log_header else 0))
     check(rc, "leveldb_crc32c_batch_host")
     return out, mm
 

@@ -290,7 +290,7 @@ int leveldb_crc32c_batch_fixed(const void* dev_base, size_t stride, size_t len, 
   if (nblocks == 0) return 0;
   if (dev_base == nullptr) return Fail(PRISMDB_CRC32C_EINVAL, "dev_base is NULL");
   if (len > 0xFFFFFFFFull) return Fail(PRISMDB_CRC32C_EINVAL, "len must be < 4 GiB");
-  if ((flags & ~(PRISMDB_CRC32C_MASK | PRISMDB_CRC32C_WRITE_TRAILER)) != 0)
+  if ((flags & ~(PRISMDB_CRC32C_MASK | PRISMDB_CRC32C_WRITE_TRAILER | PRISMDB_CRC32C_LOG_HEADER)) != 0)
     return Fail(PRISMDB_CRC32C_EINVAL, "unknown flag bits");
   if ((flags & PRISMDB_CRC32C_WRITE_TRAILER) && dev_mismatch != nullptr)
     return Fail(PRISMDB_CRC32C_EINVAL, "WRITE_TRAILER and verify are exclusive");
@@ -315,7 +315,7 @@ int leveldb_crc32c_batch(const void* dev_base, const uint64_t* dev_off, const ui
   if (n == 0) return 0;
   if (dev_base == nullptr || dev_off == nullptr || dev_len == nullptr)
     return Fail(PRISMDB_CRC32C_EINVAL, "dev_base/dev_off/dev_len must be non-NULL");
-  if ((flags & ~(PRISMDB_CRC32C_MASK | PRISMDB_CRC32C_WRITE_TRAILER)) != 0)
+  if ((flags & ~(PRISMDB_CRC32C_MASK | PRISMDB_CRC32C_WRITE_TRAILER | PRISMDB_CRC32C_LOG_HEADER)) != 0)
     return Fail(PRISMDB_CRC32C_EINVAL, "unknown flag bits");
   if ((flags & PRISMDB_CRC32C_WRITE_TRAILER) && dev_mismatch != nullptr)
     return Fail(PRISMDB_CRC32C_EINVAL, "WRITE_TRAILER and verify are exclusive");

@@ -12,6 +12,8 @@ constexpr uint32_t kConditioning = 0xFFFFFFFFu;  // util/crc32c.cc:246
 constexpr uint32_t kMaskDelta = 0xa282ead8u;     // util/crc32c.h:22
 constexpr uint32_t kFlagMask = 0x1u;             // == PRISMDB_CRC32C_MASK
 constexpr uint32_t kFlagWriteTrailer = 0x2u;     // == PRISMDB_CRC32C_WRITE_TRAILER
+constexpr uint32_t kFlagLogHeader = 0x4u;        // == PRISMDB_CRC32C_LOG_HEADER
+constexpr uint32_t kLogCrcBack = 6u;             // log record: crc sits 6 B before type||payload
 
 constexpr int kWave = 64;
 constexpr int kWavesPerGroup = 16;                 // 1024-thread workgroup, one per CU

@@ -295,6 +295,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
     const uint64_t m = *a.n_dev;
     n = m < n ? m : n;
   }
+  const bool hdr = (a.flags & kFlagLogHeader) != 0;
   bool skip_long = a.role == kRoleSpans;  // long spans go through segments...
   if (a.overflow != nullptr && *a.overflow != 0u) {
     if (a.role == kRoleSegments) n = 0;   // ...unless the segment workspace overflowed
@@ -357,8 +358,11 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
   auto issue = [&](const Task& t, uint32_t (&w)[kRounds], uint32_t& e) {
     const bool live = !t.skip;
     const uint32_t pad = t.pad(), h = t.h(), tl = t.t(), nch = t.nch(), len = t.len();
+    // Edge window: [start - hb, start + len + 4) when verifying a trailer after
+    // the span, [start - 6, start + len) when the stored crc is a log header.
+    const uint32_t hb = kVerify && hdr ? kLogCrcBack : 0u;
     u32x4 rb = buffer_rsrc(t.body(), live ? t.r.z : 0u);
-    u32x4 re = buffer_rsrc(t.start(), live ? len + (kVerify ? 4u : 0u) : 0u);
+    u32x4 re = buffer_rsrc(t.start() - hb, live ? hb + len + (kVerify && !hdr ? 4u : 0u) : 0u);
     // The descriptors may come from v_readfirstlane (VALU -> SGPR) and the
     // buffer loads read them inside asm, where hipcc inserts no wait states:
     // 5 are required (cdna_hip_programming.md 5.7 item 2).
@@ -378,9 +382,9 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
     }
     const bool first = t.c == 0, last = t.c + 1 == nch;
     uint32_t eoff = 0xFFFFFFFFu;
-    if (first && lane < h) eoff = lane;
-    if (last && lane >= 3u && lane < 3u + tl) eoff = h + t.r.z + (lane - 3u);
-    if (kVerify && last && lane >= 6u && lane < 10u) eoff = len + (lane - 6u);
+    if (first && lane < h) eoff = hb + lane;
+    if (last && lane >= 3u && lane < 3u + tl) eoff = hb + h + t.r.z + (lane - 3u);
+    if (kVerify && last && lane >= 6u && lane < 10u) eoff = (hdr ? 0u : len) + (lane - 6u);
     e = buf_ubyte(re, eoff);
   };
 
@@ -422,7 +426,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
     if (lane == 0) {
       const uint32_t res = (a.flags & kFlagMask) ? mask_crc(crc) : crc;
       if (a.out != nullptr) a.out[t.b] = res;
-      if (a.flags & kFlagWriteTrailer) store_le32(t.body() + t.r.z + tl, res);
+      if (a.flags & kFlagWriteTrailer) store_le32(hdr ? t.start() - kLogCrcBack : t.body() + t.r.z + tl, res);
       if (kVerify && a.mismatch != nullptr) {
         const uint32_t stored = readlane(e, 6) | (readlane(e, 7) << 8) | (readlane(e, 8) << 16) |
                                 (readlane(e, 9) << 24);
@@ -640,9 +644,10 @@ __global__ __launch_bounds__(256) void crc32c_combine_kernel(SpanBatch a, SplitW
     if (a.out != nullptr) a.out[span] = res;
     const uint64_t off = kDesc ? a.off[span] : span * a.stride;
     const uint32_t len = kDesc ? a.len[span] : a.len_c;
-    if (a.flags & kFlagWriteTrailer) store_le32(a.base + off + len, res);
+    const bool hdr = (a.flags & kFlagLogHeader) != 0;
+    const uint8_t* t = hdr ? a.base + off - kLogCrcBack : a.base + off + len;
+    if (a.flags & kFlagWriteTrailer) store_le32(t, res);
     if (kVerify && a.mismatch != nullptr) {
-      const uint8_t* t = a.base + off + len;
       const uint32_t stored = (uint32_t)t[0] | ((uint32_t)t[1] << 8) | ((uint32_t)t[2] << 16) |
                               ((uint32_t)t[3] << 24);
       a.mismatch[span] = crc != unmask_crc(stored) ? 1 : 0;

@@ -131,12 +131,17 @@ int leveldb_crc32c_batch_host(const void* host_base, const uint64_t* off, const 
   if (n == 0) return 0;
   if (host_base == nullptr || off == nullptr || len == nullptr)
     return PipeFail(PRISMDB_CRC32C_EINVAL, "host_base/off/len must be non-NULL");
-  if (flags & ~PRISMDB_CRC32C_MASK)
-    return PipeFail(PRISMDB_CRC32C_EINVAL, "host batches take PRISMDB_CRC32C_MASK only");
-  const size_t tail = mismatch != nullptr ? 4 : 0;  // verify reads the stored trailer
+  if (flags & ~(PRISMDB_CRC32C_MASK | PRISMDB_CRC32C_LOG_HEADER))
+    return PipeFail(PRISMDB_CRC32C_EINVAL, "host batches take PRISMDB_CRC32C_MASK and _LOG_HEADER only");
+  // Verify reads the stored checksum: the 4 bytes after the span, or with
+  // LOG_HEADER the log record header 6 bytes before it.
+  const bool hdr = (flags & PRISMDB_CRC32C_LOG_HEADER) != 0;
+  const size_t lead = mismatch != nullptr && hdr ? 6 : 0;
+  const size_t tail = mismatch != nullptr && !hdr ? 4 : 0;
   for (size_t i = 0; i < n; ++i) {
-    if ((size_t)len[i] + tail > kChunkBytes) return PipeFail(PRISMDB_CRC32C_EINVAL, "span larger than 64 MiB");
+    if (lead + (size_t)len[i] + tail > kChunkBytes) return PipeFail(PRISMDB_CRC32C_EINVAL, "span larger than 64 MiB");
     if (i && off[i] < off[i - 1]) return PipeFail(PRISMDB_CRC32C_EINVAL, "spans must be sorted by offset");
+    if (off[i] < lead) return PipeFail(PRISMDB_CRC32C_EINVAL, "log record header before the buffer start");
   }
   int rc = 0;
   Ring* ring = GetRing(rc);
@@ -161,7 +166,7 @@ int leveldb_crc32c_batch_host(const void* host_base, const uint64_t* off, const 
     Slot& s = ring->slot[k];
     if ((rc = retire(s)) != 0) return rc;
     // Chunk: consecutive spans whose bytes (plus trailers) fit kChunkBytes.
-    const uint64_t lo = off[i];
+    const uint64_t lo = off[i] - lead;
     uint64_t hi = lo;
     size_t j = i;
     while (j < n && j - i < kChunkSpans) {

@@ -13,7 +13,7 @@ from conftest import ROOT
 
 def _declared_symbols():
     names = set()
-    for h in ("prismdb_crc32c.h", "prismdb_synth.h", "prismdb_sst.h"):
+    for h in ("prismdb_crc32c.h", "prismdb_synth.h", "prismdb_sst.h", "prismdb_log.h"):
         with open(os.path.join(ROOT, "include", h)) as f:
             src = f.read()
         src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
