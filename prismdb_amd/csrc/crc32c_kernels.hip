@@ -61,12 +61,44 @@ __device__ __forceinline__ uint32_t wave_xor(uint32_t v) {
   return readlane(v, 0) ^ readlane(v, 16) ^ readlane(v, 32) ^ readlane(v, 48);
 }
 
-// One zero byte through the reflected LFSR, bit-serial (wave-uniform, SALU).
-__device__ __forceinline__ uint32_t feed_byte(uint32_t r, uint32_t byte) {
-  r ^= byte;
+// Short shifts on the vector unit.  Feeding t <= 3 bytes b0..b(t-1) into the
+// register r is shift_t(r ^ (b0 | b1 << 8 | b2 << 16)) (the word-feed identity
+// cut to t bytes), and shift_t is a 32x32 GF(2) matrix: lane i < 32 holds its
+// column i for t = 1, 2, 3 (computed once per wave, 24 LFSR steps), so
+// shift_t(x) for a wave-uniform x is one select per lane and a 32-lane XOR.
+struct ShortShift {
+  uint32_t col[3];
+};
+
+__device__ __forceinline__ ShortShift short_shift_cols(uint32_t lane) {
+  ShortShift s;
+  uint32_t c = lane < 32u ? 1u << lane : 0u;
 #pragma unroll
-  for (int k = 0; k < 8; ++k) r = (r >> 1) ^ (kPolyReflected & (0u - (r & 1u)));
-  return r;
+  for (int t = 0; t < 3; ++t) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) c = (c >> 1) ^ (kPolyReflected & (0u - (c & 1u)));
+    s.col[t] = c;
+  }
+  return s;
+}
+
+// XOR over lanes 0..31 (lanes 32..63 must hold 0 or be ignored): DPP within
+// rows, then rows 0 and 1.
+__device__ __forceinline__ uint32_t half_xor(uint32_t v) {
+  v ^= __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false);
+  v ^= __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false);
+  v ^= __builtin_amdgcn_mov_dpp(v, 0x141, 0xF, 0xF, false);
+  v ^= __builtin_amdgcn_mov_dpp(v, 0x140, 0xF, 0xF, false);
+  return readlane(v, 0) ^ readlane(v, 16);
+}
+
+// Feed the t (0..3) bytes of d (little-endian) into the uniform register r.
+__device__ __forceinline__ uint32_t feed_short(const ShortShift& ss, uint32_t lane, uint32_t r, uint32_t d,
+                                               uint32_t t) {
+  if (t == 0) return r;
+  const uint32_t x = r ^ d;
+  const uint32_t col = t == 1 ? ss.col[0] : (t == 2 ? ss.col[1] : ss.col[2]);
+  return half_xor(((x >> (lane & 31u)) & 1u) ? col : 0u);
 }
 
 // The caller owns the span's trailer bytes when it asks for them to be written
@@ -310,6 +342,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
   __syncthreads();
   const StrideLanes tab = stride_lanes(lane);
   const uint32_t* nibtab = lds + kTabWords + lane;
+  const ShortShift ss = short_shift_cols(lane);
   const uint64_t wave = rfl(blockIdx.x * kWavesPerGroup + (tid >> 6));
   const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerGroup;
   if (wave >= n) return;
@@ -395,8 +428,8 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
   auto begin = [&](int s, const Task& t, uint32_t (&w)[kRounds], uint32_t e) {
     if (t.c == 0) {
       const uint32_t h = t.h();
-      uint32_t rr = t.r.w ^ kConditioning;
-      for (uint32_t qb = 0; qb < h; ++qb) rr = feed_byte(rr, readlane(e, qb));
+      const uint32_t d = h ? readlane(e, 0) | (readlane(e, 1) << 8) | (readlane(e, 2) << 16) : 0u;
+      const uint32_t rr = feed_short(ss, lane, t.r.w ^ kConditioning, d, h);
       r[s] = rr;
       acc[s] = 0u;
       if (t.r.z) {
@@ -419,10 +452,9 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
   };
   // End of a span: tail bytes, conditioning, outputs.
   auto finish = [&](int s, const Task& t, uint32_t e, uint32_t body) {
-    uint32_t rr = t.r.z ? body : r[s];
     const uint32_t tl = t.t();
-    for (uint32_t qb = 0; qb < tl; ++qb) rr = feed_byte(rr, readlane(e, 3u + qb));
-    const uint32_t crc = rr ^ kConditioning;
+    const uint32_t d = tl ? readlane(e, 3) | (readlane(e, 4) << 8) | (readlane(e, 5) << 16) : 0u;
+    const uint32_t crc = feed_short(ss, lane, t.r.z ? body : r[s], d, tl) ^ kConditioning;
     if (lane == 0) {
       const uint32_t res = (a.flags & kFlagMask) ? mask_crc(crc) : crc;
       if (a.out != nullptr) a.out[t.b] = res;

@@ -12,6 +12,9 @@ L+4+1 per span):
   sst_desc           same spans through descriptors + one 486 977-B index span per 16 811 (split path)
   verify_4k          ReadBlock-verify of 16 Mi x (4092 + type... ) 4 KiB spans with stored trailers
   adversarial        random lengths 0..70 000 at random byte offsets (2 Mi spans over 16 GiB)
+  wal_verify         log::Reader's record check over 4096 x 4 MiB log files of ~1 KB records
+                     (PrismDB YCSB WriteBatch size), LOG_HEADER verify: L+4+1+12 per record
+  wal_seal           log::Writer's header crc for the same records, written in place: L+4+12
 """
 import argparse
 import json
@@ -111,7 +114,63 @@ def main():
     t = timed(lambda: crc32c.batch(buf, d_off, d_len, out=out3), args.reps)
     report("adversarial", t, lens.sum(), lens.sum() + 16 * m, m)
 
+    del d_off, d_len, out3
+
+    # WAL: one 4 MiB log file of ~1 KB records written in log format, tiled
+    from prismdb_amd import log
+
+    file_bytes = 4 << 20
+    nfiles = (16 << 30) // file_bytes
+    img = build_log(rng, file_bytes)
+    hoff, hlen = log.scan(img)
+    buf[:nfiles * file_bytes].view(nfiles, file_bytes).copy_(torch.from_numpy(img).to(dev))
+    base = np.arange(nfiles, dtype=np.int64)[:, None] * file_bytes
+    all_off = (base + hoff.astype(np.int64)[None, :]).reshape(-1)
+    all_len = np.tile(hlen.astype(np.int64), nfiles)
+    d_hoff = torch.from_numpy(all_off).to(dev)
+    d_hlen = torch.from_numpy(all_len.astype(np.int32)).to(dev)
+    m = len(all_off)
+    t = timed(lambda: log.seal_log(buf, d_hoff, d_hlen), args.reps)
+    report("wal_seal", t, int(all_len.sum()) + m, int(all_len.sum()) + m * (1 + 4 + 12), m)
+    d_soff, d_slen = d_hoff + 6, d_hlen + 1
+    out4 = torch.empty(m, dtype=torch.int32, device=dev)
+    mm4 = torch.empty(m, dtype=torch.uint8, device=dev)
+    t = timed(lambda: crc32c.batch(buf, d_soff, d_slen, out=out4, mismatch=mm4, verify=True, log_header=True),
+              args.reps)
+    bad = int(mm4.sum())
+    report("wal_verify", t, int(all_len.sum()) + m, int(all_len.sum()) + m * (1 + 4 + 1 + 12), m)
+    res["wal_verify"]["mismatches"] = bad
+
     print(json.dumps({"reps": args.reps, "results": res}, indent=1))
+
+
+def build_log(rng, nbytes):
+    """A log file in LevelDB's record format (db/log_format.h), ~1 KB records
+    (PrismDB YCSB WriteBatch: 980 B value + key + batch header), crc fields
+    zero (sealed on the device), cut at nbytes."""
+    import numpy as np
+
+    B, H = 32768, 7
+    out = bytearray()
+    bo = 0
+    while len(out) < nbytes:
+        left = int(rng.integers(990, 1031))
+        begin = True
+        while True:
+            if B - bo < H:
+                out += bytes(B - bo)
+                bo = 0
+            frag = min(left, B - bo - H)
+            end = frag == left
+            typ = 1 if begin and end else 2 if begin else 4 if end else 3
+            out += bytes(4) + bytes([frag & 0xFF, frag >> 8, typ]) + rng.bytes(frag)
+            bo += H + frag
+            left -= frag
+            begin = False
+            if left == 0:
+                break
+    img = np.frombuffer(bytes(out[:nbytes]), dtype=np.uint8).copy()
+    return img
 
 
 if __name__ == "__main__":

@@ -67,6 +67,26 @@ def do_run(args, names):
     ml = rng.choice([1024, 4096, 16384, 65536], size=(args.gib << 30) // 21760 // 2).astype(np.int64)
     mo = np.concatenate([[0], np.cumsum(ml)[:-1]])
     moff, mlen = torch.from_numpy(mo).to(dev), torch.from_numpy(ml.astype(np.int32)).to(dev)
+    # WAL records (~1 KB, log format) tiled over the buffer, verified with LOG_HEADER
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from bench_configs import build_log
+    from prismdb_amd import log
+
+    fb = 4 << 20
+    nf = (args.gib << 30) // fb // 4
+    img = build_log(rng, fb)
+    hoff, hlen = log.scan(img)
+    buf[:nf * fb].view(nf, fb).copy_(torch.from_numpy(img).to(dev))
+    woff = torch.from_numpy(((np.arange(nf, dtype=np.int64)[:, None] * fb + hoff.astype(np.int64)[None, :]) + 6)
+                            .reshape(-1)).to(dev)
+    wlen = torch.from_numpy(np.tile(hlen.astype(np.int32) + 1, nf)).to(dev)
+    nw = woff.numel()
+    crc32c.batch(buf, woff, wlen, mask=True, trailer=True, log_header=True)  # log::Writer's header crcs
+    wout = torch.empty(nw, dtype=torch.int32, device=dev)
+    wmm = torch.empty(nw, dtype=torch.uint8, device=dev)
+    al = rng.integers(0, 70000, size=(args.gib << 30) // 35000 // 2).astype(np.int64)
+    ao = np.sort(rng.integers(0, (args.gib << 30) // 2 - 70001, size=len(al))).astype(np.int64)
+    aoff, alen = torch.from_numpy(ao).to(dev), torch.from_numpy(al.astype(np.int32)).to(dev)
     work = {
         "fixed4k": (lambda n: libs[n][0](buf.data_ptr(), 4096, 4096, nblk, 0, out.data_ptr(), None, 0, sp),
                     nblk * 4100),
@@ -76,6 +96,11 @@ def do_run(args, names):
                                           sp), nblk * 4105),
         "mixed": (lambda n: libs[n][1](buf.data_ptr(), moff.data_ptr(), mlen.data_ptr(), None, len(ml),
                                        out.data_ptr(), None, 0, sp), int(ml.sum()) + 16 * len(ml)),
+        "wal": (lambda n: libs[n][1](buf.data_ptr(), woff.data_ptr(), wlen.data_ptr(), None, nw,
+                                     wout.data_ptr(), wmm.data_ptr(), 0x4, sp),
+                int(hlen.sum() + len(hlen)) * nf + nw * (4 + 1 + 12)),
+        "adversarial": (lambda n: libs[n][1](buf.data_ptr(), aoff.data_ptr(), alen.data_ptr(), None, len(al),
+                                             out.data_ptr(), None, 0, sp), int(al.sum()) + 16 * len(al)),
     }
 
     def timed(fn, n):
@@ -88,14 +113,25 @@ def do_run(args, names):
         return e0.elapsed_time(e1) / 1e3
 
     res = {w: {n: [] for n in names} for w in work}
+    agree = {}
+    outs_of = {"wal": wout}
     for w, (fn, _) in work.items():
+        ref = None
         for n in names:
+            o = outs_of.get(w, out)
+            o.fill_(0)
             timed(fn, n)
+            got = o.clone()
+            if ref is None:
+                ref = got
+            agree[f"{w}:{n}"] = bool(torch.equal(ref, got))
+        if w == "wal":
+            agree["wal:no_mismatch"] = int(wmm.sum()) == 0
     for _ in range(args.reps):
         for w, (fn, _) in work.items():
             for n in names:
                 res[w][n].append(timed(fn, n))
-    print(json.dumps({"gib": args.gib, "reps": args.reps,
+    print(json.dumps({"gib": args.gib, "reps": args.reps, "agree": agree,
                       "results": {w: {n: {"GB/s_median": round(work[w][1] / statistics.median(v) / 1e9, 1),
                                           "ms_median": round(statistics.median(v) * 1e3, 3)}
                                       for n, v in r.items()} for w, r in res.items()}}, indent=1))
