@@ -35,6 +35,9 @@
 
 #include "crc32c_device.h"
 
+#ifndef PRISMDB_FIXED_NOFOLD
+#define PRISMDB_FIXED_NOFOLD 0
+#endif
 #ifndef PRISMDB_RING
 #define PRISMDB_RING 4  // span buffers in the fixed kernel's prefetch ring (even)
 #endif
@@ -583,12 +586,21 @@ __global__ __launch_bounds__(kThreads) void crc32c_fixed_kernel(SpanBatch a) {
     xa ^= lane == pk ? r0 : 0u;  // initial register enters with body word 0
     xb ^= lane == pk ? r0 : 0u;
     uint32_t acc_a = xa, acc_b = xb;
+#if PRISMDB_FIXED_NOFOLD  // measurement knob: loads and stores only (wrong results)
+#pragma unroll
+    for (int j = 1; j < K; ++j) {
+      acc_a ^= wa[j];
+      acc_b ^= wb[j];
+    }
+    const uint32_t va = acc_a, vb = acc_b;
+#else
 #pragma unroll
     for (int j = 1; j < K; ++j) {
       acc_a = step256(lds, tab, acc_a, wa[j]);
       acc_b = step256(lds, tab, acc_b, wb[j]);
     }
     const uint32_t va = realign(nibtab, acc_a), vb = realign(nibtab, acc_b);
+#endif
     const uint32_t ca = wave_xor(va) ^ kConditioning, cb = wave_xor(vb) ^ kConditioning;
     const uint64_t ba = wave + k * nwaves, bb = ba + nwaves;
     if (lane == 0) {

@@ -48,3 +48,56 @@ extern "C" int bwprobe_read(const void* p, uint64_t nbytes, uint32_t* out, int w
 #undef L
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
+
+// Block pattern of the CRC kernels: each wave owns whole 4 KiB blocks
+// (16 dword loads, one per 256-B round), blocks dealt round-robin over the
+// grid's waves, kR blocks in flight per wave per iteration.  kXcd remaps
+// waves so that each XCD (workgroup b runs on XCD b % 8) reads one contiguous
+// region per step instead of 64 KiB pieces interleaved with the other XCDs.
+template <int kT, int kR, bool kXcd>
+__global__ __launch_bounds__(kT) void read_blocks(const uint8_t* __restrict__ p, uint64_t nblocks,
+                                                  uint32_t* __restrict__ out) {
+  constexpr int kWpg = kT / 64;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t nw = (uint64_t)gridDim.x * kWpg;
+  uint64_t gw;
+  if (kXcd) {
+    const uint32_t x = blockIdx.x % 8u, i = blockIdx.x / 8u;
+    gw = (uint64_t)x * (nw / 8) + (uint64_t)i * kWpg + (threadIdx.x >> 6);
+  } else {
+    gw = (uint64_t)blockIdx.x * kWpg + (threadIdx.x >> 6);
+  }
+  uint32_t acc = 0;
+  for (uint64_t k = gw; k + (uint64_t)(kR - 1) * nw < nblocks; k += (uint64_t)kR * nw) {
+    uint32_t w[kR][16];
+#pragma unroll
+    for (int r = 0; r < kR; ++r) {
+      const uint32_t* q = reinterpret_cast<const uint32_t*>(p + (k + (uint64_t)r * nw) * 4096) + lane;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) w[r][j] = __builtin_nontemporal_load(q + 64 * j);
+    }
+#pragma unroll
+    for (int r = 0; r < kR; ++r)
+#pragma unroll
+      for (int j = 0; j < 16; ++j) acc ^= w[r][j];
+  }
+  out[blockIdx.x * kT + threadIdx.x] = acc;
+}
+
+extern "C" int bwprobe_blocks(const void* p, uint64_t nblocks, uint32_t* out, int wg, int ring, int xcd, int grid,
+                              void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const uint8_t* b = (const uint8_t*)p;
+#define B(T, R, X) read_blocks<T, R, X><<<grid, T, 0, s>>>(b, nblocks, out)
+  if (wg == 1024) {
+    if (ring == 1) { if (xcd) B(1024, 1, true); else B(1024, 1, false); }
+    else if (ring == 2) { if (xcd) B(1024, 2, true); else B(1024, 2, false); }
+    else { if (xcd) B(1024, 4, true); else B(1024, 4, false); }
+  } else {
+    if (ring == 1) { if (xcd) B(256, 1, true); else B(256, 1, false); }
+    else if (ring == 2) { if (xcd) B(256, 2, true); else B(256, 2, false); }
+    else { if (xcd) B(256, 4, true); else B(256, 4, false); }
+  }
+#undef B
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}

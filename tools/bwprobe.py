@@ -33,6 +33,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gib", type=int, default=16)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--blocks-only", action="store_true", help="block-pattern probes + dword nt grid-stride only")
     args = ap.parse_args()
     build()
     import torch
@@ -57,9 +58,19 @@ def main():
         e1.synchronize()
         return e0.elapsed_time(e1) / 1e3
 
+    probe.bwprobe_blocks.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                     ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
     variants = {}
-    for width in (4, 8, 16):
-        for nt in (0, 1):
+    sp = ctypes.c_void_p(stream.cuda_stream)
+    nb = nbytes // 4096
+    for wg, grid in ((1024, 256), (256, 1024), (256, 2048)):
+        for ring in (1, 2, 4):
+            for xcd in (0, 1):
+                key = f"blocks_wg{wg}_g{grid}_r{ring}_x{xcd}"
+                variants[key] = (lambda w=wg, g=grid, r=ring, x=xcd: probe.bwprobe_blocks(
+                    buf.data_ptr(), nb, out.data_ptr(), w, r, x, g, sp), nb * 4096)
+    for width in ((4,) if args.blocks_only else (4, 8, 16)):
+        for nt in ((1,) if args.blocks_only else (0, 1)):
             for grid in (1024, 2048, 4096, 8192):
                 key = f"read_w{width}_nt{nt}_g{grid}"
                 variants[key] = (lambda w=width, t=nt, g=grid: probe.bwprobe_read(

@@ -21,6 +21,9 @@ VDIR = os.path.join(ROOT, "tools", "_build", "variants")
 
 VARIANTS = {
     "base": {"PRISMDB_RING": 4, "PRISMDB_NT_LOADS": 1},
+    # measurement-only: fixed kernel without the CRC fold (loads + stores), wrong results
+    "nofold": {"PRISMDB_FIXED_NOFOLD": 1},
+    "nofold_nt0": {"PRISMDB_FIXED_NOFOLD": 1, "PRISMDB_NT_LOADS": 0},
 }
 # Libraries built elsewhere (e.g. from an older commit in a git worktree) and
 # dropped into VDIR as lib_<name>.so join the comparison with --only <name>.
