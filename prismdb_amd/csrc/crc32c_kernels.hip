@@ -35,6 +35,9 @@
 
 #include "crc32c_device.h"
 
+#ifndef PRISMDB_FIXED_NOSTORE  // measurement knob: no result stores (wrong results)
+#define PRISMDB_FIXED_NOSTORE 0
+#endif
 #ifndef PRISMDB_FIXED_NOFOLD
 #define PRISMDB_FIXED_NOFOLD 0
 #endif
@@ -348,8 +351,22 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
   const ShortShift ss = short_shift_cols(lane);
   const uint64_t wave = rfl(blockIdx.x * kWavesPerGroup + (tid >> 6));
   const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerGroup;
-  if (wave >= n) return;
-  const uint64_t step = 2 * nwaves;
+  // Spans are dealt in runs of kRun consecutive records per stream: run r of
+  // stream s of wave w is records [((r * nwaves + w) * 2 + s) * kRun, +kRun).
+  // Lane i of res[s] / bad[s] collects the run's i-th result / verify flag,
+  // stored with one coalesced nt store per run (scattered 4-byte stores cost
+  // 10 % of the read rate; the fixed kernel's comment has the measurement).
+  // kRun = 64, shortened so every stream gets >= 16 runs: with spans of mixed
+  // sizes, fewer and longer runs leave the last ones unbalanced (config 3 and
+  // the adversarial mix lost 4 % at >= 4 runs), and long spans make the
+  // per-span store a small share anyway.
+  uint32_t lg = 6;
+  while (lg > 0 && (n >> (lg + 1)) < nwaves * 16u) --lg;
+  const uint64_t kRun = 1ull << lg;
+  if ((wave << (lg + 1)) >= n) return;
+  auto next_rec = [&](uint64_t k) -> uint64_t {  // the stream's record after k
+    return ((k + 1) & (kRun - 1)) ? k + 1 : k + 1 + (2 * nwaves - 1) * kRun;
+  };
 
   auto read_rec = [&](uint64_t b) -> SpanRec {
     SpanRec r{0u, 0u, 0u, 0u};
@@ -385,7 +402,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
     for (int s = 0; s < 2; ++s) {
       if (refill[s]) {
         refill[s] = false;
-        pend_b[s] += step;
+        pend_b[s] = next_rec(pend_b[s]);
         pend[s] = read_rec(pend_b[s]);
       }
     }
@@ -453,20 +470,33 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
       }
     }
   };
+  // Run results: flush lanes [0, kRun) of stream s's run starting at record base.
+  uint32_t res[2] = {0u, 0u}, bad[2] = {0u, 0u};
+  uint64_t unflushed[2] = {~0ull, ~0ull};  // base record of a run holding unstored results
+  auto flush = [&](int s, uint64_t base) {
+    if (lane < kRun && base + lane < n) {
+      if (a.out != nullptr) __builtin_nontemporal_store(res[s], a.out + base + lane);
+      if (kVerify && a.mismatch != nullptr) __builtin_nontemporal_store((uint8_t)bad[s], a.mismatch + base + lane);
+    }
+  };
   // End of a span: tail bytes, conditioning, outputs.
   auto finish = [&](int s, const Task& t, uint32_t e, uint32_t body) {
     const uint32_t tl = t.t();
     const uint32_t d = tl ? readlane(e, 3) | (readlane(e, 4) << 8) | (readlane(e, 5) << 16) : 0u;
     const uint32_t crc = feed_short(ss, lane, t.r.z ? body : r[s], d, tl) ^ kConditioning;
-    if (lane == 0) {
-      const uint32_t res = (a.flags & kFlagMask) ? mask_crc(crc) : crc;
-      if (a.out != nullptr) a.out[t.b] = res;
-      if (a.flags & kFlagWriteTrailer) store_le32(hdr ? t.start() - kLogCrcBack : t.body() + t.r.z + tl, res);
-      if (kVerify && a.mismatch != nullptr) {
-        const uint32_t stored = readlane(e, 6) | (readlane(e, 7) << 8) | (readlane(e, 8) << 16) |
-                                (readlane(e, 9) << 24);
-        a.mismatch[t.b] = crc != unmask_crc(stored) ? 1 : 0;
-      }
+    const uint32_t v = (a.flags & kFlagMask) ? mask_crc(crc) : crc;
+    const uint32_t slot = (uint32_t)(t.b & (kRun - 1));
+    res[s] = lane == slot ? v : res[s];
+    if (kVerify) {
+      const uint32_t stored = readlane(e, 6) | (readlane(e, 7) << 8) | (readlane(e, 8) << 16) | (readlane(e, 9) << 24);
+      bad[s] = lane == slot ? (crc != unmask_crc(stored) ? 1u : 0u) : bad[s];
+    }
+    if ((a.flags & kFlagWriteTrailer) && lane == 0)
+      store_le32(hdr ? t.start() - kLogCrcBack : t.body() + t.r.z + tl, v);
+    unflushed[s] = t.b - slot;
+    if (slot == kRun - 1) {
+      flush(s, t.b - slot);
+      unflushed[s] = ~0ull;
     }
   };
   // Fold the pair (stream 0 task tx in wx, stream 1 task ty in wy).
@@ -504,9 +534,9 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
   uint32_t eb[2][2];
 #pragma unroll
   for (int st = 0; st < 2; ++st) {
-    const uint64_t b0 = wave + (uint64_t)st * nwaves;
+    const uint64_t b0 = (2 * wave + st) * kRun;
     tk[0][st] = make_task(b0, read_rec(b0));
-    pend_b[st] = b0 + step;
+    pend_b[st] = next_rec(b0);
     pend[st] = read_rec(pend_b[st]);
   }
   tk[1][0] = next_task(0, tk[0][0]);
@@ -533,6 +563,10 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
     }
   }
 drained:
+  // Partial last runs: every record < n of them is done.
+#pragma unroll
+  for (int st = 0; st < 2; ++st)
+    if (unflushed[st] != ~0ull) flush(st, unflushed[st]);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
@@ -541,8 +575,8 @@ drained:
 // base, stride and len multiples of 4 and len <= 4 KiB, so a span is K rounds
 // (K = ceil(len/256), a template parameter) with no head/tail bytes and the
 // same padding (pk = 64K - len/4 leading zero words, all in round 0).
-// Straight-line ring of three span buffers (loop unrolled x3): the loads of
-// span k+2 are in flight while span k is folded; counted vmcnt waits only.
+// Ring of four span buffers consumed in pairs (loop unrolled x2): the next
+// pair's loads are in flight while a pair is folded; counted vmcnt waits only.
 // ---------------------------------------------------------------------------
 template <int K>
 __global__ __launch_bounds__(kThreads) void crc32c_fixed_kernel(SpanBatch a) {
@@ -557,7 +591,24 @@ __global__ __launch_bounds__(kThreads) void crc32c_fixed_kernel(SpanBatch a) {
   const uint32_t* nibtab = lds + kTabWords + lane;
   const uint64_t wave = rfl(blockIdx.x * kWavesPerGroup + (tid >> 6));
   const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerGroup;
-  if (wave >= n) return;
+
+  // Spans are dealt to waves in runs of kRun consecutive spans: run r of wave
+  // w is spans [(r * nwaves + w) * kRun, +kRun), two per pair step.  Lane i
+  // of `res` collects the run's i-th result and the run ends with ONE
+  // coalesced 256-B store.  (One 4-byte store per span, scattered over 4096
+  // waves, cost 10 % of the read rate in partial-line writes -- measured
+  // with tools/bwprobe.py's store-pattern probes, profiles/
+  // r01_bwprobe_store_patterns.json; runs of 64 also read 2-4 % faster than
+  // spans dealt one by one.)
+  // kRun = 64, shortened (power of two >= 2) for batches too small to give
+  // every wave a few full runs.
+  uint32_t lg = 5;  // log2(pair steps per run)
+  while (lg > 0 && (n >> (lg + 1)) < nwaves * 4u) --lg;
+  const uint32_t kSteps = 1u << lg, kRun = 2u * kSteps;
+  auto span_of = [&](uint64_t t) -> uint64_t {  // first span of pair step t
+    return (((t >> lg) * nwaves + wave) << (lg + 1)) + 2u * (t & (kSteps - 1u));
+  };
+  if (span_of(0) >= n) return;
 
   const uint32_t pk = 64u * K - (a.len_c >> 2);  // 0..63 leading zero words (round 0)
   const uint32_t r0 = a.init_c ^ kConditioning;
@@ -570,16 +621,18 @@ __global__ __launch_bounds__(kThreads) void crc32c_fixed_kernel(SpanBatch a) {
   // counted waits (hipcc's own waitcnt pass merges the ring's scoreboards into
   // vmcnt(0), which would drain the prefetch).  Unconditional: a span past the
   // end re-reads the last one.  Every buffer is exactly K loads.
-  auto issue = [&](uint64_t k, uint32_t (&w)[kRounds]) {
-    uint64_t b = wave + k * nwaves;
+  auto issue = [&](uint64_t b, uint32_t (&w)[kRounds]) {
     b = b < n ? b : n - 1;
     const uint8_t* p = a.base + b * a.stride;
     w[0] = asm_load_dword<0>(p, off0);
 #pragma unroll
     for (int j = 1; j < K; ++j) w[j] = asm_load_dword_at<K>(p, off1, j);
   };
+  uint32_t res = 0;
   // Two spans folded together: two independent LDS dependency chains per wave.
-  auto fold2 = [&](uint64_t k, uint32_t (&wa)[kRounds], uint32_t (&wb)[kRounds]) {
+  // The waits count only the ring's loads: the run-end store, when younger
+  // than the awaited loads, only makes a wait stricter.
+  auto fold2 = [&](uint64_t t, uint32_t (&wa)[kRounds], uint32_t (&wb)[kRounds]) {
     wait_ring<(kRing - 2) * K>(wa);  // the younger pair may stay in flight
     wait_ring<(kRing - 2) * K>(wb);
     uint32_t xa = lane >= pk ? wa[0] : 0u, xb = lane >= pk ? wb[0] : 0u;
@@ -602,11 +655,17 @@ __global__ __launch_bounds__(kThreads) void crc32c_fixed_kernel(SpanBatch a) {
     const uint32_t va = realign(nibtab, acc_a), vb = realign(nibtab, acc_b);
 #endif
     const uint32_t ca = wave_xor(va) ^ kConditioning, cb = wave_xor(vb) ^ kConditioning;
-    const uint64_t ba = wave + k * nwaves, bb = ba + nwaves;
-    if (lane == 0) {
-      a.out[ba] = masked ? mask_crc(ca) : ca;
-      if (bb < n) a.out[bb] = masked ? mask_crc(cb) : cb;
-    }
+    const uint32_t i = 2u * (uint32_t)(t & (kSteps - 1u));
+    res = lane == i ? (masked ? mask_crc(ca) : ca) : res;
+    res = lane == i + 1u ? (masked ? mask_crc(cb) : cb) : res;
+  };
+  // Run end (or the last pair): lanes 0..i+1 hold results of spans b0 + lane.
+  auto flush = [&](uint64_t t) {
+    const uint64_t b0 = span_of(t) - 2u * (t & (kSteps - 1u));
+    const uint32_t last = 2u * (uint32_t)(t & (kSteps - 1u)) + 1u;
+    // nt: the results are not re-read; a streaming store keeps them from
+    // contending with the read stream (0.6 % of the read rate vs 2 %, probes).
+    if (!PRISMDB_FIXED_NOSTORE && lane <= last && b0 + lane < n) __builtin_nontemporal_store(res, a.out + b0 + lane);
   };
 
   // Ring of kRing span buffers, consumed in pairs; loop unrolled so every
@@ -615,14 +674,24 @@ __global__ __launch_bounds__(kThreads) void crc32c_fixed_kernel(SpanBatch a) {
   static_assert((kRing - 2) * K <= 63, "vmcnt is a 6-bit counter");
   uint32_t ring[kRing][kRounds];
 #pragma unroll
-  for (int d = 0; d < kRing; ++d) issue(d, ring[d]);
-  for (uint64_t k = 0;; k += kRing) {
+  for (int d = 0; d < kRing; d += 2) {
+    const uint64_t b = span_of(d / 2);
+    issue(b, ring[d]);
+    issue(b + 1, ring[d + 1]);
+  }
+  for (uint64_t t = 0;; t += kRing / 2) {
 #pragma unroll
     for (int s = 0; s < kRing; s += 2) {
-      fold2(k + s, ring[s], ring[s + 1]);
-      if (wave + (k + s + 2) * nwaves >= n) goto drained;
-      issue(k + s + kRing, ring[s]);
-      issue(k + s + kRing + 1, ring[s + 1]);
+      const uint64_t ts = t + s / 2;
+      fold2(ts, ring[s], ring[s + 1]);
+      const uint64_t nb = span_of(ts + kRing / 2);  // the pair this slot refills
+      if (span_of(ts + 1) >= n) {
+        flush(ts);
+        goto drained;
+      }
+      if (((ts + 1) & (kSteps - 1u)) == 0) flush(ts);
+      issue(nb, ring[s]);
+      issue(nb + 1, ring[s + 1]);
     }
   }
 drained:

@@ -69,6 +69,18 @@ def main():
                 key = f"blocks_wg{wg}_g{grid}_r{ring}_x{xcd}"
                 variants[key] = (lambda w=wg, g=grid, r=ring, x=xcd: probe.bwprobe_blocks(
                     buf.data_ptr(), nb, out.data_ptr(), w, r, x, g, sp), nb * 4096)
+    probe.bwprobe_blocks_store.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int,
+                                           ctypes.c_int, ctypes.c_void_p]
+    res_out = torch.empty(nb, dtype=torch.int32, device=dev)
+    for mode in range(7):
+        variants[f"blocks_store_mode{mode}"] = (lambda md=mode: probe.bwprobe_blocks_store(
+            buf.data_ptr(), nb, res_out.data_ptr(), md, 256, sp), nb * 4096)
+    probe.bwprobe_runs_store.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int,
+                                         ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+    for mode, params in ((0, (128, 256, 512)), (1, (2, 4, 8)), (2, (0,))):
+        for prm in params:
+            variants[f"runs_store_m{mode}_p{prm}"] = (lambda md=mode, pr=prm: probe.bwprobe_runs_store(
+                buf.data_ptr(), nb, res_out.data_ptr(), md, pr, 256, sp), nb * 4096)
     for width in ((4,) if args.blocks_only else (4, 8, 16)):
         for nt in ((1,) if args.blocks_only else (0, 1)):
             for grid in (1024, 2048, 4096, 8192):

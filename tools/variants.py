@@ -24,6 +24,8 @@ VARIANTS = {
     # measurement-only: fixed kernel without the CRC fold (loads + stores), wrong results
     "nofold": {"PRISMDB_FIXED_NOFOLD": 1},
     "nofold_nt0": {"PRISMDB_FIXED_NOFOLD": 1, "PRISMDB_NT_LOADS": 0},
+    "nostore": {"PRISMDB_FIXED_NOSTORE": 1},
+    "nofold_nostore": {"PRISMDB_FIXED_NOFOLD": 1, "PRISMDB_FIXED_NOSTORE": 1},
 }
 # Libraries built elsewhere (e.g. from an older commit in a git worktree) and
 # dropped into VDIR as lib_<name>.so join the comparison with --only <name>.
