@@ -47,6 +47,15 @@
 #ifndef PRISMDB_NT_LOADS
 #define PRISMDB_NT_LOADS 1  // body words are read once: non-temporal
 #endif
+#ifndef PRISMDB_XOR3
+#define PRISMDB_XOR3 1  // three-input XORs through v_bitop3_b32
+#endif
+#ifndef PRISMDB_EARLY
+#define PRISMDB_EARLY 0  // fixed kernel: issue the next pair before folding the landed one (needs RING >= 6)
+#endif
+#ifndef PRISMDB_RUN_LG
+#define PRISMDB_RUN_LG 5  // fixed kernel: log2(pair steps per run); runs of 2 << PRISMDB_RUN_LG spans
+#endif
 
 namespace prismdb {
 namespace dev {
@@ -152,6 +161,15 @@ __device__ __forceinline__ uint32_t lds_word(const uint32_t* lds, uint32_t byte_
   return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(lds) + byte_addr);
 }
 
+// a ^ b ^ c in one VALU instruction (gfx950 v_bitop3_b32, truth table 0x96).
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+#if PRISMDB_XOR3
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+#else
+  return a ^ b ^ c;
+#endif
+}
+
 // One stream step: shift_256(acc) ^ w with four conflict-free LDS lookups
 // (w is folded in early so only one XOR trails the last lookup).
 __device__ __forceinline__ uint32_t step256(const uint32_t* lds, const StrideLanes& t, uint32_t acc,
@@ -160,17 +178,26 @@ __device__ __forceinline__ uint32_t step256(const uint32_t* lds, const StrideLan
   const uint32_t a1 = lds_word(lds, __builtin_amdgcn_perm(acc, t.L[1], 0x0C020500u));
   const uint32_t a2 = lds_word(lds, __builtin_amdgcn_perm(acc, t.L[2], 0x0C020600u));
   const uint32_t a3 = lds_word(lds, __builtin_amdgcn_perm(acc, t.L[3], 0x0C020700u));
-  const uint32_t x = w ^ a0 ^ a1;
-  return x ^ a2 ^ a3;
+  return xor3(xor3(w, a0, a1), a2, a3);
 }
 
 // shift_{256-4l}(acc) for this lane: eight nibble lookups in lane l's own
-// tables (entry [n][v] at word 64*(16n+v)+l, so bank = l mod 32).
-__device__ __forceinline__ uint32_t realign(const uint32_t* __restrict__ nibtab, uint32_t acc) {
-  uint32_t v = 0;
+// tables (entry [n][v] at word 64*(16n+v)+l, so bank = l mod 32).  nib is the
+// byte address of lane l's entry [0][0] (bits 2-7 and 17 only), so each
+// address is one shift plus one v_and_or_b32, the table offset n*4 KiB rides
+// in the instruction's offset field.
+__device__ __forceinline__ uint32_t nib_addr(uint32_t acc, int n, uint32_t nib) {
+  const uint32_t x = n < 2 ? acc << (8 - 4 * n) : acc >> (4 * n - 8);
+  uint32_t a;  // (x & 0xF00) | nib in one instruction (hipcc prefers and + add)
+  asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(a) : "v"(x), "s"(0xF00u), "v"(nib));
+  return a;
+}
+
+__device__ __forceinline__ uint32_t realign(const uint32_t* lds, uint32_t nib, uint32_t acc) {
+  uint32_t v[8];
 #pragma unroll
-  for (int n = 0; n < 8; ++n) v ^= nibtab[(uint32_t)(16 * n) * 64u + (((acc >> (4 * n)) & 15u) << 6)];
-  return v;
+  for (int n = 0; n < 8; ++n) v[n] = lds_word(lds, nib_addr(acc, n, nib) + 4096u * n);
+  return xor3(xor3(v[0], v[1], v[2]), xor3(v[3], v[4], v[5]), v[6] ^ v[7]);
 }
 
 }  // namespace
@@ -347,7 +374,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
   const uint32_t lane = tid & 63u;
   __syncthreads();
   const StrideLanes tab = stride_lanes(lane);
-  const uint32_t* nibtab = lds + kTabWords + lane;
+  const uint32_t nibtab = 4u * (kTabWords + lane);  // byte address of lane's nibble entry [0][0]
   const ShortShift ss = short_shift_cols(lane);
   const uint64_t wave = rfl(blockIdx.x * kWavesPerGroup + (tid >> 6));
   const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerGroup;
@@ -514,14 +541,14 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
     acc[1] = ay;
     const bool endx = !tx.skip && tx.c + 1 == tx.nch(), endy = !ty.skip && ty.c + 1 == ty.nch();
     if (endx && endy) {
-      const uint32_t vx = realign(nibtab, ax), vy = realign(nibtab, ay);
+      const uint32_t vx = realign(lds, nibtab, ax), vy = realign(lds, nibtab, ay);
       const uint32_t bx = wave_xor(vx), by = wave_xor(vy);
       finish(0, tx, ex, bx);
       finish(1, ty, ey, by);
     } else if (endx) {
-      finish(0, tx, ex, wave_xor(realign(nibtab, ax)));
+      finish(0, tx, ex, wave_xor(realign(lds, nibtab, ax)));
     } else if (endy) {
-      finish(1, ty, ey, wave_xor(realign(nibtab, ay)));
+      finish(1, ty, ey, wave_xor(realign(lds, nibtab, ay)));
     }
   };
 
@@ -563,11 +590,17 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
     }
   }
 drained:
-  // Partial last runs: every record < n of them is done.
+  // Retire the abandoned slot's loads while their registers are live (see the
+  // fixed kernel's drain), then store the partial last runs: every record < n
+  // of them is done.
+#pragma unroll
+  for (int sl = 0; sl < 2; ++sl) {
+    wait_task<0>(wb[sl][0], eb[sl][0]);
+    wait_task<0>(wb[sl][1], eb[sl][1]);
+  }
 #pragma unroll
   for (int st = 0; st < 2; ++st)
     if (unflushed[st] != ~0ull) flush(st, unflushed[st]);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 // ---------------------------------------------------------------------------
@@ -588,7 +621,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_fixed_kernel(SpanBatch a) {
   const uint32_t lane = tid & 63u;
   __syncthreads();
   const StrideLanes tab = stride_lanes(lane);
-  const uint32_t* nibtab = lds + kTabWords + lane;
+  const uint32_t nibtab = 4u * (kTabWords + lane);  // byte address of lane's nibble entry [0][0]
   const uint64_t wave = rfl(blockIdx.x * kWavesPerGroup + (tid >> 6));
   const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerGroup;
 
@@ -602,7 +635,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_fixed_kernel(SpanBatch a) {
   // spans dealt one by one.)
   // kRun = 64, shortened (power of two >= 2) for batches too small to give
   // every wave a few full runs.
-  uint32_t lg = 5;  // log2(pair steps per run)
+  uint32_t lg = PRISMDB_RUN_LG;  // log2(pair steps per run)
   while (lg > 0 && (n >> (lg + 1)) < nwaves * 4u) --lg;
   const uint32_t kSteps = 1u << lg, kRun = 2u * kSteps;
   auto span_of = [&](uint64_t t) -> uint64_t {  // first span of pair step t
@@ -632,9 +665,14 @@ __global__ __launch_bounds__(kThreads) void crc32c_fixed_kernel(SpanBatch a) {
   // Two spans folded together: two independent LDS dependency chains per wave.
   // The waits count only the ring's loads: the run-end store, when younger
   // than the awaited loads, only makes a wait stricter.
-  auto fold2 = [&](uint64_t t, uint32_t (&wa)[kRounds], uint32_t (&wb)[kRounds]) {
-    wait_ring<(kRing - 2) * K>(wa);  // the younger pair may stay in flight
-    wait_ring<(kRing - 2) * K>(wb);
+  // Pairs issued after the one being waited for: all the others (refill after
+  // the fold) or all but one (EARLY: the free slot is refilled before the fold).
+  constexpr int kYounger = (kRing / 2 - 1 - PRISMDB_EARLY) * 2 * K;
+  auto wait2 = [&](uint32_t (&wa)[kRounds], uint32_t (&wb)[kRounds]) {
+    wait_ring<kYounger>(wa);  // the younger pairs may stay in flight
+    wait_ring<kYounger>(wb);
+  };
+  auto fold2 = [&](uint64_t t, const uint32_t (&wa)[kRounds], const uint32_t (&wb)[kRounds]) {
     uint32_t xa = lane >= pk ? wa[0] : 0u, xb = lane >= pk ? wb[0] : 0u;
     xa ^= lane == pk ? r0 : 0u;  // initial register enters with body word 0
     xb ^= lane == pk ? r0 : 0u;
@@ -652,7 +690,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_fixed_kernel(SpanBatch a) {
       acc_a = step256(lds, tab, acc_a, wa[j]);
       acc_b = step256(lds, tab, acc_b, wb[j]);
     }
-    const uint32_t va = realign(nibtab, acc_a), vb = realign(nibtab, acc_b);
+    const uint32_t va = realign(lds, nibtab, acc_a), vb = realign(lds, nibtab, acc_b);
 #endif
     const uint32_t ca = wave_xor(va) ^ kConditioning, cb = wave_xor(vb) ^ kConditioning;
     const uint32_t i = 2u * (uint32_t)(t & (kSteps - 1u));
@@ -670,32 +708,54 @@ __global__ __launch_bounds__(kThreads) void crc32c_fixed_kernel(SpanBatch a) {
 
   // Ring of kRing span buffers, consumed in pairs; loop unrolled so every
   // buffer has a static register name.
-  static_assert(kRing % 2 == 0 && kRing >= 4, "the fixed kernel folds spans in pairs, one pair in flight");
-  static_assert((kRing - 2) * K <= 63, "vmcnt is a 6-bit counter");
+  static_assert(kRing % 2 == 0 && kRing >= 4 + 2 * PRISMDB_EARLY, "pairs; one pair in flight during a fold");
+  static_assert(kYounger <= 63, "vmcnt is a 6-bit counter");
+  constexpr int kAhead = kRing / 2 - PRISMDB_EARLY;  // pairs issued before the first fold
   uint32_t ring[kRing][kRounds];
 #pragma unroll
-  for (int d = 0; d < kRing; d += 2) {
+  for (int d = 0; d < 2 * kAhead; d += 2) {
     const uint64_t b = span_of(d / 2);
     issue(b, ring[d]);
     issue(b + 1, ring[d + 1]);
   }
+  // One exit, at the bottom of a whole ring turn: steps past the wave's last
+  // pair (their loads re-read span n-1) are waited for but not folded.  The
+  // prefetched pairs still in flight at the exit are retired while their
+  // registers are live (operands of the markers after the wait), so the
+  // compiler cannot hand such a register to other code before its load lands.
   for (uint64_t t = 0;; t += kRing / 2) {
 #pragma unroll
     for (int s = 0; s < kRing; s += 2) {
       const uint64_t ts = t + s / 2;
-      fold2(ts, ring[s], ring[s + 1]);
-      const uint64_t nb = span_of(ts + kRing / 2);  // the pair this slot refills
-      if (span_of(ts + 1) >= n) {
-        flush(ts);
-        goto drained;
+      const uint64_t nb = span_of(ts + kAhead);  // the next pair to issue
+      wait2(ring[s], ring[s + 1]);
+#if PRISMDB_EARLY
+      // Refill the slot folded in the previous step before folding this one:
+      // kAhead pairs stay in flight through the fold.  Every slot keeps a
+      // static register name (loop unrolled over the ring), so no in-flight
+      // register is ever copied.
+      const int f = (s + kRing - 2) % kRing;  // compile-time after unrolling
+      issue(nb, ring[f]);
+      issue(nb + 1, ring[f + 1]);
+#endif
+      if (span_of(ts) < n) {
+        fold2(ts, ring[s], ring[s + 1]);
+        if (span_of(ts + 1) >= n || ((ts + 1) & (kSteps - 1u)) == 0) flush(ts);
       }
-      if (((ts + 1) & (kSteps - 1u)) == 0) flush(ts);
+#if !PRISMDB_EARLY
       issue(nb, ring[s]);
       issue(nb + 1, ring[s + 1]);
+#endif
     }
+    if (span_of(t + kRing / 2) >= n) break;
   }
-drained:
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the ring's extra prefetches
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int d = 0; d < kRing; ++d) {
+    if (PRISMDB_EARLY && d >= kRing - 2) continue;  // EARLY: the last slot folded has landed
+#pragma unroll
+    for (int j = 0; j < K; ++j) asm volatile("" : "+v"(ring[d][j]));
+  }
 }
 
 // ---------------------------------------------------------------------------
