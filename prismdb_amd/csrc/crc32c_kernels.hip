@@ -50,9 +50,6 @@
 #ifndef PRISMDB_XOR3
 #define PRISMDB_XOR3 1  // three-input XORs through v_bitop3_b32
 #endif
-#ifndef PRISMDB_EARLY
-#define PRISMDB_EARLY 0  // fixed kernel: issue the next pair before folding the landed one (needs RING >= 6)
-#endif
 #ifndef PRISMDB_RUN_LG
 #define PRISMDB_RUN_LG 5  // fixed kernel: log2(pair steps per run); runs of 2 << PRISMDB_RUN_LG spans
 #endif
@@ -67,12 +64,26 @@ __device__ __forceinline__ uint32_t readlane(uint32_t x, uint32_t l) {
   return __builtin_amdgcn_readlane(x, l);
 }
 
+// v ^ dpp(v): with every lane active and bound_ctrl set, hipcc fuses the pair
+// into one v_xor_b32_dpp.
+__device__ __forceinline__ uint32_t xor_dpp(uint32_t v, int ctrl) {
+  switch (ctrl) {
+    case 0xB1: return v ^ __builtin_amdgcn_update_dpp(0u, v, 0xB1, 0xF, 0xF, true);
+    case 0x4E: return v ^ __builtin_amdgcn_update_dpp(0u, v, 0x4E, 0xF, 0xF, true);
+    case 0x141: return v ^ __builtin_amdgcn_update_dpp(0u, v, 0x141, 0xF, 0xF, true);
+    default: return v ^ __builtin_amdgcn_update_dpp(0u, v, 0x140, 0xF, 0xF, true);
+  }
+}
+
+// XOR within each row of 16 lanes: quad_perm [1,0,3,2], quad_perm [2,3,0,1],
+// row_half_mirror, row_mirror.
+__device__ __forceinline__ uint32_t row_xor(uint32_t v) {
+  return xor_dpp(xor_dpp(xor_dpp(xor_dpp(v, 0xB1), 0x4E), 0x141), 0x140);
+}
+
 // XOR of v over the 64 lanes (wave-uniform result).
 __device__ __forceinline__ uint32_t wave_xor(uint32_t v) {
-  v ^= __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
-  v ^= __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
-  v ^= __builtin_amdgcn_mov_dpp(v, 0x141, 0xF, 0xF, false);  // row_half_mirror
-  v ^= __builtin_amdgcn_mov_dpp(v, 0x140, 0xF, 0xF, false);  // row_mirror
+  v = row_xor(v);
   return readlane(v, 0) ^ readlane(v, 16) ^ readlane(v, 32) ^ readlane(v, 48);
 }
 
@@ -100,10 +111,7 @@ __device__ __forceinline__ ShortShift short_shift_cols(uint32_t lane) {
 // XOR over lanes 0..31 (lanes 32..63 must hold 0 or be ignored): DPP within
 // rows, then rows 0 and 1.
 __device__ __forceinline__ uint32_t half_xor(uint32_t v) {
-  v ^= __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false);
-  v ^= __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false);
-  v ^= __builtin_amdgcn_mov_dpp(v, 0x141, 0xF, 0xF, false);
-  v ^= __builtin_amdgcn_mov_dpp(v, 0x140, 0xF, 0xF, false);
+  v = row_xor(v);
   return readlane(v, 0) ^ readlane(v, 16);
 }
 
@@ -635,13 +643,16 @@ __global__ __launch_bounds__(kThreads) void crc32c_fixed_kernel(SpanBatch a) {
   // spans dealt one by one.)
   // kRun = 64, shortened (power of two >= 2) for batches too small to give
   // every wave a few full runs.
+  static_assert(PRISMDB_RUN_LG >= 0 && PRISMDB_RUN_LG <= 5, "a run's results fit the 64 lanes");
   uint32_t lg = PRISMDB_RUN_LG;  // log2(pair steps per run)
   while (lg > 0 && (n >> (lg + 1)) < nwaves * 4u) --lg;
-  const uint32_t kSteps = 1u << lg, kRun = 2u * kSteps;
-  auto span_of = [&](uint64_t t) -> uint64_t {  // first span of pair step t
-    return (((t >> lg) * nwaves + wave) << (lg + 1)) + 2u * (t & (kSteps - 1u));
-  };
-  if (span_of(0) >= n) return;
+  const uint64_t kRun = 2ull << lg;
+  // First span of the wave's next pair step: +2 inside a run, then on to the
+  // wave's next run (the other waves' runs in between).
+  const uint64_t jump = (nwaves - 1u) * kRun + 2u;
+  auto adv = [&](uint64_t x) -> uint64_t { return ((x + 2u) & (kRun - 1u)) ? x + 2u : x + jump; };
+  uint64_t cur = wave * kRun;  // first span of the pair being folded
+  if (cur >= n) return;
 
   const uint32_t pk = 64u * K - (a.len_c >> 2);  // 0..63 leading zero words (round 0)
   const uint32_t r0 = a.init_c ^ kConditioning;
@@ -663,16 +674,14 @@ __global__ __launch_bounds__(kThreads) void crc32c_fixed_kernel(SpanBatch a) {
   };
   uint32_t res = 0;
   // Two spans folded together: two independent LDS dependency chains per wave.
-  // The waits count only the ring's loads: the run-end store, when younger
-  // than the awaited loads, only makes a wait stricter.
-  // Pairs issued after the one being waited for: all the others (refill after
-  // the fold) or all but one (EARLY: the free slot is refilled before the fold).
-  constexpr int kYounger = (kRing / 2 - 1 - PRISMDB_EARLY) * 2 * K;
+  // The waits count only the ring's loads (the pairs issued after the awaited
+  // one); the run-end store, when younger than them, only makes a wait stricter.
+  constexpr int kYounger = (kRing / 2 - 1) * 2 * K;
   auto wait2 = [&](uint32_t (&wa)[kRounds], uint32_t (&wb)[kRounds]) {
     wait_ring<kYounger>(wa);  // the younger pairs may stay in flight
     wait_ring<kYounger>(wb);
   };
-  auto fold2 = [&](uint64_t t, const uint32_t (&wa)[kRounds], const uint32_t (&wb)[kRounds]) {
+  auto fold2 = [&](const uint32_t (&wa)[kRounds], const uint32_t (&wb)[kRounds]) {
     uint32_t xa = lane >= pk ? wa[0] : 0u, xb = lane >= pk ? wb[0] : 0u;
     xa ^= lane == pk ? r0 : 0u;  // initial register enters with body word 0
     xb ^= lane == pk ? r0 : 0u;
@@ -693,66 +702,56 @@ __global__ __launch_bounds__(kThreads) void crc32c_fixed_kernel(SpanBatch a) {
     const uint32_t va = realign(lds, nibtab, acc_a), vb = realign(lds, nibtab, acc_b);
 #endif
     const uint32_t ca = wave_xor(va) ^ kConditioning, cb = wave_xor(vb) ^ kConditioning;
-    const uint32_t i = 2u * (uint32_t)(t & (kSteps - 1u));
+    const uint32_t i = (uint32_t)(cur & (kRun - 1u));  // the pair's lanes in the run
     res = lane == i ? (masked ? mask_crc(ca) : ca) : res;
     res = lane == i + 1u ? (masked ? mask_crc(cb) : cb) : res;
   };
   // Run end (or the last pair): lanes 0..i+1 hold results of spans b0 + lane.
-  auto flush = [&](uint64_t t) {
-    const uint64_t b0 = span_of(t) - 2u * (t & (kSteps - 1u));
-    const uint32_t last = 2u * (uint32_t)(t & (kSteps - 1u)) + 1u;
+  auto flush = [&]() {
+    const uint64_t b0 = cur & ~(kRun - 1u);
+    const uint32_t last = (uint32_t)(cur & (kRun - 1u)) + 1u;
     // nt: the results are not re-read; a streaming store keeps them from
     // contending with the read stream (0.6 % of the read rate vs 2 %, probes).
     if (!PRISMDB_FIXED_NOSTORE && lane <= last && b0 + lane < n) __builtin_nontemporal_store(res, a.out + b0 + lane);
   };
 
   // Ring of kRing span buffers, consumed in pairs; loop unrolled so every
-  // buffer has a static register name.
-  static_assert(kRing % 2 == 0 && kRing >= 4 + 2 * PRISMDB_EARLY, "pairs; one pair in flight during a fold");
+  // buffer has a static register name.  (Refilling a slot before its fold,
+  // with a 6-buffer ring, measured no faster: profiles/r01_variants_ring_runs.json.)
+  static_assert(kRing % 2 == 0 && kRing >= 4, "pairs; one pair in flight during a fold");
   static_assert(kYounger <= 63, "vmcnt is a 6-bit counter");
-  constexpr int kAhead = kRing / 2 - PRISMDB_EARLY;  // pairs issued before the first fold
   uint32_t ring[kRing][kRounds];
+  uint64_t ahead = cur;  // first span of the next pair to issue
 #pragma unroll
-  for (int d = 0; d < 2 * kAhead; d += 2) {
-    const uint64_t b = span_of(d / 2);
-    issue(b, ring[d]);
-    issue(b + 1, ring[d + 1]);
+  for (int d = 0; d < kRing; d += 2) {
+    issue(ahead, ring[d]);
+    issue(ahead + 1, ring[d + 1]);
+    ahead = adv(ahead);
   }
   // One exit, at the bottom of a whole ring turn: steps past the wave's last
   // pair (their loads re-read span n-1) are waited for but not folded.  The
   // prefetched pairs still in flight at the exit are retired while their
   // registers are live (operands of the markers after the wait), so the
   // compiler cannot hand such a register to other code before its load lands.
-  for (uint64_t t = 0;; t += kRing / 2) {
+  for (;;) {
 #pragma unroll
     for (int s = 0; s < kRing; s += 2) {
-      const uint64_t ts = t + s / 2;
-      const uint64_t nb = span_of(ts + kAhead);  // the next pair to issue
       wait2(ring[s], ring[s + 1]);
-#if PRISMDB_EARLY
-      // Refill the slot folded in the previous step before folding this one:
-      // kAhead pairs stay in flight through the fold.  Every slot keeps a
-      // static register name (loop unrolled over the ring), so no in-flight
-      // register is ever copied.
-      const int f = (s + kRing - 2) % kRing;  // compile-time after unrolling
-      issue(nb, ring[f]);
-      issue(nb + 1, ring[f + 1]);
-#endif
-      if (span_of(ts) < n) {
-        fold2(ts, ring[s], ring[s + 1]);
-        if (span_of(ts + 1) >= n || ((ts + 1) & (kSteps - 1u)) == 0) flush(ts);
+      const uint64_t nxt = adv(cur);
+      if (cur < n) {
+        fold2(ring[s], ring[s + 1]);
+        if (nxt >= n || (nxt & (kRun - 1u)) == 0) flush();
       }
-#if !PRISMDB_EARLY
-      issue(nb, ring[s]);
-      issue(nb + 1, ring[s + 1]);
-#endif
+      cur = nxt;
+      issue(ahead, ring[s]);
+      issue(ahead + 1, ring[s + 1]);
+      ahead = adv(ahead);
     }
-    if (span_of(t + kRing / 2) >= n) break;
+    if (cur >= n) break;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
   for (int d = 0; d < kRing; ++d) {
-    if (PRISMDB_EARLY && d >= kRing - 2) continue;  // EARLY: the last slot folded has landed
 #pragma unroll
     for (int j = 0; j < K; ++j) asm volatile("" : "+v"(ring[d][j]));
   }

@@ -256,6 +256,34 @@ def test_full_size_config2_properties(dev, oracle):
     torch.cuda.empty_cache()
 
 
+@pytest.mark.parametrize("nblk,length", [((1 << 20) + 37, 4096), ((1 << 20) + 127, 4092), ((1 << 20) + 1, 2048)])
+def test_fixed_full_runs_partial_tail(dev, oracle, nblk, length):
+    """Batches big enough for the fixed kernel's full 64-span runs, with a
+    partial last run: every block against the descriptor path, the last
+    run-and-a-half plus random samples against the oracle."""
+    import torch
+    from prismdb_amd import crc32c
+
+    L = 4096
+    buf = torch.empty(nblk * L, dtype=torch.uint8, device=dev)
+    crc32c.fill_synthetic(buf, SEED)
+    out, _ = crc32c.batch_fixed(buf, L, length, nblk, init=0xABCDEF01, mask=True)
+    off = torch.arange(nblk, dtype=torch.int64, device=dev) * L
+    lens = torch.full((nblk,), length, dtype=torch.int32, device=dev)
+    init = torch.full((nblk,), 0xABCDEF01 - (1 << 32), dtype=torch.int32, device=dev)
+    out2, _ = crc32c.batch(buf, off, lens, init, mask=True)
+    assert torch.equal(out, out2)
+    rng = np.random.default_rng(2)
+    idx = np.unique(np.concatenate([np.arange(nblk - 200, nblk), rng.integers(0, nblk, 512)]))
+    got = _u32(out[torch.from_numpy(idx).to(dev)])
+    for j, i in enumerate(idx.tolist()):
+        host = oracle.synth(length, SEED, i * L)
+        want = oracle.batch_fixed(host, length, length, 1, init=0xABCDEF01, mask=True)[0]
+        assert got[j] == want, i
+    del buf, off, lens, init, out, out2
+    torch.cuda.empty_cache()
+
+
 def test_concurrent_streams(dev, oracle):
     """Two streams in flight at once give the same answers as one."""
     import torch

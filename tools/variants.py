@@ -26,12 +26,11 @@ VARIANTS = {
     "nofold_nt0": {"PRISMDB_FIXED_NOFOLD": 1, "PRISMDB_NT_LOADS": 0},
     "nostore": {"PRISMDB_FIXED_NOSTORE": 1},
     "nofold_nostore": {"PRISMDB_FIXED_NOFOLD": 1, "PRISMDB_FIXED_NOSTORE": 1},
-    # fixed kernel: next pair issued before the fold, 3 pairs in registers
-    "early6": {"PRISMDB_EARLY": 1, "PRISMDB_RING": 6},
-    # fixed kernel: runs of 16 / 256 spans per wave instead of 64
+    # fixed kernel: runs of 16 spans per wave instead of 64
     "run3": {"PRISMDB_RUN_LG": 3},
-    "run7": {"PRISMDB_RUN_LG": 7},
 }
+# Measured and dropped (profiles/r01_variants_ring_runs.json): refilling a ring
+# pair before its fold with a 6-buffer ring ("early6") was no faster.
 # Libraries built elsewhere (e.g. from an older commit in a git worktree) and
 # dropped into VDIR as lib_<name>.so join the comparison with --only <name>.
 
