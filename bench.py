@@ -147,8 +147,8 @@ def load_pmc_traffic(nblocks: int):
 
 def e2e_leg(args, torch, crc32c, dev) -> dict:
     """Host-resident rate through leveldb_crc32c_batch_host: 4 KiB blocks in
-    host memory streamed H2D -> CRC -> results D2H in 64 MiB chunks, 3 in
-    flight.  Measured for a pinned source (direct DMA) and a pageable one
+    host memory streamed H2D -> CRC -> results D2H in 32 MiB chunks, 4 in
+    flight on separate copy and compute streams.  Measured for a pinned source (direct DMA) and a pageable one
     (staged through the engine's pinned ring), next to the plain pinned H2D
     copy rate of the same bytes.  Never the headline value."""
     import numpy as np
@@ -162,20 +162,27 @@ def e2e_leg(args, torch, crc32c, dev) -> dict:
     lens = np.full(nblk, BLOCK, dtype=np.uint32)
     ref, _ = crc32c.batch_fixed(tmp, BLOCK, BLOCK, nblk)
     ref = ref.cpu().numpy().view(np.uint32)
-    res = {"bytes": nblk * BLOCK, "chunk": "64 MiB, 3 in flight"}
+    res = {"bytes": nblk * BLOCK, "chunk": "32 MiB per DMA, 4 in flight, copy and compute streams",
+           "reps": 3, "stat": "best of reps"}
     for name, src in (("pinned", pinned), ("pageable", pageable)):
         crc32c.batch_host(src, off[:16384], lens[:16384])  # warm the ring
-        t0 = time.perf_counter()
-        got, _ = crc32c.batch_host(src, off, lens)
-        t = time.perf_counter() - t0
-        res[name] = round(nblk * BLOCK / t / GIB, 2)
-        res[name + "_bit_exact"] = bool((got == ref).all())
+        best, exact = 0.0, True
+        for _ in range(3):
+            t0 = time.perf_counter()
+            got, _ = crc32c.batch_host(src, off, lens)
+            best = max(best, nblk * BLOCK / (time.perf_counter() - t0) / GIB)
+            exact = exact and bool((got == ref).all())
+        res[name] = round(best, 2)
+        res[name + "_bit_exact"] = exact
     d = torch.empty_like(tmp)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    d.copy_(pinned, non_blocking=True)
-    torch.cuda.synchronize()
-    res["h2d_copy_only"] = round(nblk * BLOCK / (time.perf_counter() - t0) / GIB, 2)
+    best = 0.0
+    for _ in range(3):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        d.copy_(pinned, non_blocking=True)
+        torch.cuda.synchronize()
+        best = max(best, nblk * BLOCK / (time.perf_counter() - t0) / GIB)
+    res["h2d_copy_only"] = round(best, 2)
     res["unit"] = "GiB/s"
     return res
 

@@ -3,19 +3,28 @@
 // PrismDB's blocks start and end in host memory: SST file pages read with
 // pread during compaction (util/env_posix.cc:172-208) and blocks appended to a
 // 32 MiB write buffer (:279-309).  leveldb_crc32c_batch_host streams such a
-// batch through the device: spans are cut into chunks of <= kChunkBytes of
-// consecutive file bytes; each chunk goes host -> (pinned staging, if the
-// source is pageable) -> H2D -> batch kernel -> D2H of the 4-byte results, on
-// kDepth streams so copies in both directions overlap the kernels.  The call
-// is synchronous (like ReadBlock) and thread-safe: every calling thread gets
-// its own staging ring per device.
+// batch through the device.  Spans are cut into chunks of <= kChunkBytes of
+// consecutive file bytes, and the work is split over two streams so the PCIe
+// link never idles:
+//   copy stream     chunk bytes host -> device, back to back (the bottleneck);
+//   compute stream  per chunk: descriptors H2D (one packed copy), wait for the
+//                   chunk's bytes, batch kernels, 4-byte results D2H.
+// kDepth chunks are in flight; the host refills a slot once the compute
+// stream has released it.  A pageable source is first staged into the slot's
+// pinned buffer by several host threads (one memcpy thread reaches about half
+// the link rate).  The call is synchronous (like ReadBlock) and thread-safe:
+// every calling thread gets its own ring per device.
 #include <hip/hip_runtime.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/prismdb_crc32c.h"
@@ -26,9 +35,11 @@ void SetLastError(const std::string& msg);  // crc32c_capi.hip: leveldb_crc32c_l
 
 namespace {
 
-constexpr size_t kChunkBytes = 64ull << 20;  // one 64 MiB SST (include/leveldb/options.h:117)
+constexpr size_t kChunkBytes = 32ull << 20;  // per DMA; ~0.6 ms of PCIe Gen5 x16
+constexpr size_t kMaxSpan = 64ull << 20;     // one 64 MiB SST (include/leveldb/options.h:117)
+constexpr size_t kSlotBytes = kMaxSpan + 8;  // a chunk holds one span of up to kMaxSpan
 constexpr size_t kChunkSpans = 1u << 16;     // descriptors per chunk
-constexpr int kDepth = 3;
+constexpr int kDepth = 4;
 
 int PipeFail(int code, const std::string& msg) {
   prismdb::SetLastError(msg);
@@ -36,67 +47,74 @@ int PipeFail(int code, const std::string& msg) {
 }
 
 struct Slot {
-  hipStream_t stream = nullptr;
-  hipEvent_t done = nullptr;
-  uint8_t* h_stage = nullptr;  // pinned, kChunkBytes + 8
-  uint8_t* d_data = nullptr;   // kChunkBytes + 8
-  uint64_t* h_off = nullptr;   // pinned descriptors
-  uint32_t* h_len = nullptr;
-  uint32_t* h_init = nullptr;
-  uint64_t* d_off = nullptr;
-  uint32_t* d_len = nullptr;
-  uint32_t* d_init = nullptr;
+  hipEvent_t copied = nullptr;  // chunk bytes on the device (copy stream)
+  hipEvent_t done = nullptr;    // results on the host, slot free (compute stream)
+  uint8_t* h_stage = nullptr;   // pinned, kSlotBytes (pageable sources)
+  uint8_t* d_data = nullptr;    // kSlotBytes
+  uint8_t* h_desc = nullptr;    // pinned: off[cnt] | len[cnt] | init[cnt]
+  uint8_t* d_desc = nullptr;
   uint32_t* d_out = nullptr;
   uint8_t* d_mm = nullptr;
-  uint32_t* h_out = nullptr;   // pinned results
+  uint32_t* h_out = nullptr;  // pinned results
   uint8_t* h_mm = nullptr;
-  // pending chunk
   bool busy = false;
   size_t first = 0, count = 0;
 };
 
 struct Ring {
+  hipStream_t copy = nullptr, compute = nullptr;
   Slot slot[kDepth];
-  bool ok = false;
   ~Ring() {
+    if (copy) hipStreamSynchronize(copy);
+    if (compute) hipStreamSynchronize(compute);
     for (Slot& s : slot) {
-      if (s.stream) hipStreamSynchronize(s.stream);
       hipHostFree(s.h_stage);
-      hipHostFree(s.h_off);
+      hipHostFree(s.h_desc);
       hipHostFree(s.h_out);
       hipFree(s.d_data);
-      hipFree(s.d_off);
+      hipFree(s.d_desc);
+      if (s.copied) hipEventDestroy(s.copied);
       if (s.done) hipEventDestroy(s.done);
-      if (s.stream) hipStreamDestroy(s.stream);
     }
+    if (copy) hipStreamDestroy(copy);
+    if (compute) hipStreamDestroy(compute);
   }
 };
 
 int MakeRing(Ring& r) {
+  hipError_t e = hipStreamCreateWithFlags(&r.copy, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&r.compute, hipStreamNonBlocking);
   for (Slot& s : r.slot) {
-    hipError_t e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&s.copied, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&s.done, hipEventDisableTiming);
-    if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(&s.h_stage), kChunkBytes + 8);
-    if (e == hipSuccess)
-      e = hipHostMalloc(reinterpret_cast<void**>(&s.h_off), kChunkSpans * (8 + 4 + 4));
+    if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(&s.h_stage), kSlotBytes);
+    if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(&s.h_desc), kChunkSpans * 16);
     if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(&s.h_out), kChunkSpans * (4 + 1));
-    if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&s.d_data), kChunkBytes + 8);
-    if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&s.d_off), kChunkSpans * (8 + 4 + 4 + 4 + 1));
-    if (e != hipSuccess) return PipeFail(PRISMDB_CRC32C_EDEVICE, std::string("pipeline setup: ") + hipGetErrorString(e));
-    s.h_len = reinterpret_cast<uint32_t*>(s.h_off + kChunkSpans);
-    s.h_init = s.h_len + kChunkSpans;
+    if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&s.d_data), kSlotBytes);
+    if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&s.d_desc), kChunkSpans * (16 + 4 + 1));
+    if (e != hipSuccess) break;
     s.h_mm = reinterpret_cast<uint8_t*>(s.h_out + kChunkSpans);
-    s.d_len = reinterpret_cast<uint32_t*>(s.d_off + kChunkSpans);
-    s.d_init = s.d_len + kChunkSpans;
-    s.d_out = s.d_init + kChunkSpans;
+    s.d_out = reinterpret_cast<uint32_t*>(s.d_desc + kChunkSpans * 16);
     s.d_mm = reinterpret_cast<uint8_t*>(s.d_out + kChunkSpans);
   }
-  r.ok = true;
+  if (e != hipSuccess) return PipeFail(PRISMDB_CRC32C_EDEVICE, std::string("pipeline setup: ") + hipGetErrorString(e));
   return 0;
 }
 
+// A worker thread's rings are released when it exits.  The main thread's are
+// left to the OS: its thread-local destructors run inside exit(), where the
+// HIP runtime (or a profiler wrapped around it) may already be tearing down.
+struct RingMap {
+  std::map<int, std::unique_ptr<Ring>> rings;
+  ~RingMap() {
+    if (syscall(SYS_gettid) == getpid())
+      for (auto& kv : rings) (void)kv.second.release();
+  }
+};
+
 Ring* GetRing(int& rc) {
-  thread_local std::map<int, std::unique_ptr<Ring>> rings;
+  thread_local RingMap map;
+  std::map<int, std::unique_ptr<Ring>>& rings = map.rings;
   int dev = 0;
   hipGetDevice(&dev);
   std::unique_ptr<Ring>& r = rings[dev];
@@ -121,6 +139,39 @@ bool IsPinned(const void* p) {
   return a.type == hipMemoryTypeHost;
 }
 
+// Staging threads for pageable sources: PRISMDB_STAGE_THREADS, else half the
+// cores this process may use, capped at 8.
+int StageThreads() {
+  static const int n = [] {
+    if (const char* e = std::getenv("PRISMDB_STAGE_THREADS")) {
+      const int v = std::atoi(e);
+      if (v >= 1) return std::min(v, 64);
+    }
+    const int hw = (int)std::thread::hardware_concurrency();
+    return std::max(1, std::min(8, hw / 2));
+  }();
+  return n;
+}
+
+void ParallelCopy(uint8_t* dst, const uint8_t* src, size_t bytes) {
+  const int t = bytes >= (4u << 20) ? StageThreads() : 1;
+  if (t <= 1) {
+    std::memcpy(dst, src, bytes);
+    return;
+  }
+  const size_t piece = ((bytes + t - 1) / t + 4095) & ~size_t(4095);
+  std::vector<std::thread> th;
+  th.reserve(t - 1);
+  for (int k = 1; k < t; ++k) {
+    const size_t lo = k * piece;
+    if (lo >= bytes) break;
+    const size_t len = std::min(piece, bytes - lo);
+    th.emplace_back([=] { std::memcpy(dst + lo, src + lo, len); });
+  }
+  std::memcpy(dst, src, std::min(piece, bytes));
+  for (std::thread& x : th) x.join();
+}
+
 }  // namespace
 
 extern "C" {
@@ -139,7 +190,7 @@ int leveldb_crc32c_batch_host(const void* host_base, const uint64_t* off, const 
   const size_t lead = mismatch != nullptr && hdr ? 6 : 0;
   const size_t tail = mismatch != nullptr && !hdr ? 4 : 0;
   for (size_t i = 0; i < n; ++i) {
-    if (lead + (size_t)len[i] + tail > kChunkBytes) return PipeFail(PRISMDB_CRC32C_EINVAL, "span larger than 64 MiB");
+    if (lead + (size_t)len[i] + tail > kMaxSpan) return PipeFail(PRISMDB_CRC32C_EINVAL, "span larger than 64 MiB");
     if (i && off[i] < off[i - 1]) return PipeFail(PRISMDB_CRC32C_EINVAL, "spans must be sorted by offset");
     if (off[i] < lead) return PipeFail(PRISMDB_CRC32C_EINVAL, "log record header before the buffer start");
   }
@@ -149,7 +200,8 @@ int leveldb_crc32c_batch_host(const void* host_base, const uint64_t* off, const 
   const uint8_t* src = static_cast<const uint8_t*>(host_base);
   const bool pinned = IsPinned(host_base);
 
-  // Retire a slot: wait for its stream, hand its results to the caller.
+  // Retire a slot: wait until the compute stream released it, hand its
+  // results to the caller.
   auto retire = [&](Slot& s) -> int {
     if (!s.busy) return 0;
     hipError_t e = hipEventSynchronize(s.done);
@@ -165,39 +217,47 @@ int leveldb_crc32c_batch_host(const void* host_base, const uint64_t* off, const 
   while (i < n) {
     Slot& s = ring->slot[k];
     if ((rc = retire(s)) != 0) return rc;
-    // Chunk: consecutive spans whose bytes (plus trailers) fit kChunkBytes.
+    // Chunk: consecutive spans whose bytes (plus trailers) fit kChunkBytes;
+    // a single span may be larger (up to kMaxSpan).
     const uint64_t lo = off[i] - lead;
     uint64_t hi = lo;
     size_t j = i;
     while (j < n && j - i < kChunkSpans) {
       const uint64_t end = std::max<uint64_t>(hi, off[j] + len[j] + tail);
-      if (end - lo > kChunkBytes) break;
+      if (j > i && end - lo > kChunkBytes) break;
       hi = end;
       ++j;
     }
     const size_t cnt = j - i;
+    uint64_t* h_off = reinterpret_cast<uint64_t*>(s.h_desc);
+    uint32_t* h_len = reinterpret_cast<uint32_t*>(h_off + cnt);
+    uint32_t* h_init = h_len + cnt;
     for (size_t q = 0; q < cnt; ++q) {
-      s.h_off[q] = off[i + q] - lo;
-      s.h_len[q] = len[i + q];
-      s.h_init[q] = init ? init[i + q] : 0u;
+      h_off[q] = off[i + q] - lo;
+      h_len[q] = len[i + q];
     }
+    if (init) std::memcpy(h_init, init + i, cnt * 4);
     const size_t bytes = (size_t)(hi - lo);
     const uint8_t* from = src + lo;
     if (!pinned) {
-      std::memcpy(s.h_stage, from, bytes);  // pageable source: stage through pinned memory
+      ParallelCopy(s.h_stage, from, bytes);  // pageable source: stage through pinned memory
       from = s.h_stage;
     }
-    hipError_t e = hipMemcpyAsync(s.d_data, from, bytes, hipMemcpyHostToDevice, s.stream);
-    if (e == hipSuccess) e = hipMemcpyAsync(s.d_off, s.h_off, cnt * 8, hipMemcpyHostToDevice, s.stream);
-    if (e == hipSuccess) e = hipMemcpyAsync(s.d_len, s.h_len, cnt * 4, hipMemcpyHostToDevice, s.stream);
-    if (e == hipSuccess && init) e = hipMemcpyAsync(s.d_init, s.h_init, cnt * 4, hipMemcpyHostToDevice, s.stream);
+    const uint64_t* d_off = reinterpret_cast<const uint64_t*>(s.d_desc);
+    const uint32_t* d_len = reinterpret_cast<const uint32_t*>(d_off + cnt);
+    const uint32_t* d_init = d_len + cnt;
+    hipError_t e = hipMemcpyAsync(s.d_data, from, bytes, hipMemcpyHostToDevice, ring->copy);
+    if (e == hipSuccess) e = hipEventRecord(s.copied, ring->copy);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(s.d_desc, s.h_desc, cnt * (init ? 16 : 12), hipMemcpyHostToDevice, ring->compute);
+    if (e == hipSuccess) e = hipStreamWaitEvent(ring->compute, s.copied, 0);
     if (e != hipSuccess) return PipeFail(PRISMDB_CRC32C_EDEVICE, std::string("pipeline H2D: ") + hipGetErrorString(e));
-    rc = leveldb_crc32c_batch(s.d_data, s.d_off, s.d_len, init ? s.d_init : nullptr, cnt, s.d_out,
-                              mismatch ? s.d_mm : nullptr, flags, s.stream);
+    rc = leveldb_crc32c_batch(s.d_data, d_off, d_len, init ? d_init : nullptr, cnt, s.d_out,
+                              mismatch ? s.d_mm : nullptr, flags, ring->compute);
     if (rc != 0) return rc;  // message already set by leveldb_crc32c_batch
-    e = hipMemcpyAsync(s.h_out, s.d_out, cnt * 4, hipMemcpyDeviceToHost, s.stream);
-    if (e == hipSuccess && mismatch) e = hipMemcpyAsync(s.h_mm, s.d_mm, cnt, hipMemcpyDeviceToHost, s.stream);
-    if (e == hipSuccess) e = hipEventRecord(s.done, s.stream);
+    e = hipMemcpyAsync(s.h_out, s.d_out, cnt * 4, hipMemcpyDeviceToHost, ring->compute);
+    if (e == hipSuccess && mismatch) e = hipMemcpyAsync(s.h_mm, s.d_mm, cnt, hipMemcpyDeviceToHost, ring->compute);
+    if (e == hipSuccess) e = hipEventRecord(s.done, ring->compute);
     if (e != hipSuccess) return PipeFail(PRISMDB_CRC32C_EDEVICE, std::string("pipeline D2H: ") + hipGetErrorString(e));
     s.busy = true;
     s.first = i;
@@ -205,8 +265,8 @@ int leveldb_crc32c_batch_host(const void* host_base, const uint64_t* off, const 
     i = j;
     k = (k + 1) % kDepth;
   }
-  for (Slot& s : ring->slot)
-    if ((rc = retire(s)) != 0) return rc;
+  for (int q = 0; q < kDepth; ++q)
+    if ((rc = retire(ring->slot[(k + q) % kDepth])) != 0) return rc;
   return 0;
 }
 

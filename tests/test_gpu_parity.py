@@ -333,3 +333,30 @@ def test_host_resident_pipeline(dev, oracle):
     host[12345 * 3992 + 7] ^= 1
     _, mm = crc32c.batch_host(host, off, lens, verify=True)
     assert np.nonzero(mm)[0].tolist() == [12345]
+
+
+def test_host_pipeline_mixed_large_spans(dev, oracle):
+    """Host batches whose spans straddle the 32 MiB DMA chunk size: small
+    spans, a 48 MiB span (its own chunk), a 64 MiB - 4 span verified with its
+    trailer, then small spans again; with per-span init."""
+    from prismdb_amd import crc32c
+
+    lens = [3988] * 300 + [48 << 20, 1000, (64 << 20) - 4] + [4096] * 300 + [7, 0, 1]
+    off, pos = [], 16
+    for ln in lens:
+        off.append(pos)
+        pos += ln + 4 + (pos % 7)
+    host = oracle.synth(pos + 64, 0x5EED000E)
+    off = np.asarray(off, dtype=np.uint64)
+    lens = np.asarray(lens, dtype=np.uint32)
+    init = (np.arange(len(lens), dtype=np.uint64) * 0x9E3779B1 % (1 << 32)).astype(np.uint32)
+    want, _ = oracle.batch(host, off, lens, init)
+    got, _ = crc32c.batch_host(host, off, lens, init)
+    np.testing.assert_array_equal(got, want)
+    plain, _ = oracle.batch(host, off, lens)
+    for i in range(len(lens)):
+        o = int(off[i]) + int(lens[i])
+        host[o:o + 4] = np.frombuffer(int(oracle.mask(int(plain[i]))).to_bytes(4, "little"), dtype=np.uint8)
+    host[int(off[302]) + 12345678] ^= 0x10
+    _, mm = crc32c.batch_host(host, off, lens, verify=True)
+    assert np.nonzero(mm)[0].tolist() == [302]
