@@ -227,11 +227,15 @@ int RunBatch(DeviceCtx& ctx, const SpanBatch& base_args, bool desc, bool verify,
   SpanBatch a = base_args;
   a.tabs = ctx.tabs;
   a.role = prismdb::dev::kRoleSpans;
-  // Fast path: fixed stride, 4-byte aligned, 4..4096-byte multiple-of-4 spans.
-  if (!desc && !verify && a.out != nullptr && (a.flags & prismdb::dev::kFlagWriteTrailer) == 0 &&
-      a.len_c >= 4 && a.len_c <= 4u * prismdb::dev::kChunkWords && (a.len_c & 3u) == 0 &&
+  // Fast path: fixed stride, 4-byte aligned, 4..4096-byte multiple-of-4 spans
+  // (verify: up to 4092 bytes and not a multiple of 256, so that the stored
+  // trailer word fits round 0's padding lanes).
+  const uint32_t max_len = 4u * prismdb::dev::kChunkWords - (verify ? 4u : 0u);
+  if (!desc && (verify || a.out != nullptr) && (!verify || (a.len_c & 255u) != 0) &&
+      (a.flags & (prismdb::dev::kFlagWriteTrailer | prismdb::dev::kFlagLogHeader)) == 0 &&
+      a.len_c >= 4 && a.len_c <= max_len && (a.len_c & 3u) == 0 &&
       (a.stride & 3u) == 0 && (reinterpret_cast<uintptr_t>(a.base) & 3u) == 0 && !g_force_generic) {
-    hipError_t e = prismdb::dev::launch_fixed(a, ctx.cus, s);
+    hipError_t e = prismdb::dev::launch_fixed(a, verify, ctx.cus, s);
     return e == hipSuccess ? 0 : FailHip(e, "fixed kernel launch");
   }
   SplitWs ws{};

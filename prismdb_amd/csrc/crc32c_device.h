@@ -80,7 +80,7 @@ struct SplitWs {
 };
 
 hipError_t launch_span(const SpanBatch& a, bool verify, int grid, hipStream_t s);
-hipError_t launch_fixed(const SpanBatch& a, int grid, hipStream_t s);
+hipError_t launch_fixed(const SpanBatch& a, bool verify, int grid, hipStream_t s);
 hipError_t launch_plan(const SpanBatch& a, bool desc, const SplitWs& ws, hipStream_t s);
 hipError_t launch_combine(const SpanBatch& a, bool desc, bool verify, const SplitWs& ws,
                           hipStream_t s);

@@ -25,7 +25,8 @@
 //     issued with inline asm one pair ahead and retired by counted vmcnt.
 //
 // Kernels:
-//   crc32c_fixed_kernel<K>  fixed stride, 4-B aligned, len <= 4 KiB (config 2)
+//   crc32c_fixed_kernel<K, verify>  fixed stride, 4-B aligned, len <= 4 KiB (config 2);
+//                           verify: the stored trailer word rides in round 0
 //   crc32c_plan_kernel      one thread per span: 16-byte span records (all
 //                           geometry precomputed), long spans cut into segments
 //   crc32c_span_kernel      everything else, driven by the span records
@@ -619,7 +620,7 @@ drained:
 // Ring of four span buffers consumed in pairs (loop unrolled x2): the next
 // pair's loads are in flight while a pair is folded; counted vmcnt waits only.
 // ---------------------------------------------------------------------------
-template <int K>
+template <int K, bool kVerify>
 __global__ __launch_bounds__(kThreads) void crc32c_fixed_kernel(SpanBatch a) {
   constexpr int kRing = PRISMDB_RING;
   const uint64_t n = a.n;
@@ -654,11 +655,14 @@ __global__ __launch_bounds__(kThreads) void crc32c_fixed_kernel(SpanBatch a) {
   uint64_t cur = wave * kRun;  // first span of the pair being folded
   if (cur >= n) return;
 
-  const uint32_t pk = 64u * K - (a.len_c >> 2);  // 0..63 leading zero words (round 0)
+  // pk: leading zero words (round 0).  Verify sizes K for len + 4, so pk >= 1
+  // and lane 0 of round 0 -- padding, masked out of the fold -- loads the
+  // stored trailer word right after the span (ReadBlock, table/format.cc:93-95).
+  const uint32_t pk = 64u * K - (a.len_c >> 2);  // 0..63 (1..64 when verifying)
   const uint32_t r0 = a.init_c ^ kConditioning;
   const bool masked = (a.flags & kFlagMask) != 0;
   const int32_t w0 = (int32_t)lane - (int32_t)pk;   // word index of round 0
-  const uint32_t off0 = (uint32_t)(w0 < 0 ? 0 : w0) * 4u;
+  const uint32_t off0 = kVerify && lane == 0u ? a.len_c : (uint32_t)(w0 < 0 ? 0 : w0) * 4u;
   const uint32_t off1 = (uint32_t)(w0 + 64) * 4u;   // rounds >= 1 never clamp
 
   // The ring's loads are issued with inline asm and retired with explicit
@@ -672,7 +676,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_fixed_kernel(SpanBatch a) {
 #pragma unroll
     for (int j = 1; j < K; ++j) w[j] = asm_load_dword_at<K>(p, off1, j);
   };
-  uint32_t res = 0;
+  uint32_t res = 0, bad = 0;
   // Two spans folded together: two independent LDS dependency chains per wave.
   // The waits count only the ring's loads (the pairs issued after the awaited
   // one); the run-end store, when younger than them, only makes a wait stricter.
@@ -705,6 +709,12 @@ __global__ __launch_bounds__(kThreads) void crc32c_fixed_kernel(SpanBatch a) {
     const uint32_t i = (uint32_t)(cur & (kRun - 1u));  // the pair's lanes in the run
     res = lane == i ? (masked ? mask_crc(ca) : ca) : res;
     res = lane == i + 1u ? (masked ? mask_crc(cb) : cb) : res;
+    if (kVerify) {
+      const uint32_t ba = ca != unmask_crc(readlane(wa[0], 0)) ? 1u : 0u;
+      const uint32_t bb = cb != unmask_crc(readlane(wb[0], 0)) ? 1u : 0u;
+      bad = lane == i ? ba : bad;
+      bad = lane == i + 1u ? bb : bad;
+    }
   };
   // Run end (or the last pair): lanes 0..i+1 hold results of spans b0 + lane.
   auto flush = [&]() {
@@ -712,7 +722,10 @@ __global__ __launch_bounds__(kThreads) void crc32c_fixed_kernel(SpanBatch a) {
     const uint32_t last = (uint32_t)(cur & (kRun - 1u)) + 1u;
     // nt: the results are not re-read; a streaming store keeps them from
     // contending with the read stream (0.6 % of the read rate vs 2 %, probes).
-    if (!PRISMDB_FIXED_NOSTORE && lane <= last && b0 + lane < n) __builtin_nontemporal_store(res, a.out + b0 + lane);
+    if (!PRISMDB_FIXED_NOSTORE && lane <= last && b0 + lane < n) {
+      if (!kVerify || a.out != nullptr) __builtin_nontemporal_store(res, a.out + b0 + lane);
+      if (kVerify && a.mismatch != nullptr) __builtin_nontemporal_store((uint8_t)bad, a.mismatch + b0 + lane);
+    }
   };
 
   // Ring of kRing span buffers, consumed in pairs; loop unrolled so every
@@ -836,12 +849,14 @@ hipError_t launch_span(const SpanBatch& a, bool verify, int grid, hipStream_t s)
   return hipGetLastError();
 }
 
-hipError_t launch_fixed(const SpanBatch& a, int grid, hipStream_t s) {
-  const int rounds = (int)((a.len_c + 255u) / 256u);  // 1..16
+hipError_t launch_fixed(const SpanBatch& a, bool verify, int grid, hipStream_t s) {
+  // rounds: ceil(len / 256), or ceil((len + 4) / 256) when the trailer rides along
+  const int rounds = (int)((a.len_c + (verify ? 4u : 0u) + 255u) / 256u);  // 1..16
   switch (rounds) {
-#define PRISMDB_CASE(K) \
-  case K:               \
-    crc32c_fixed_kernel<K><<<grid, kThreads, 0, s>>>(a); \
+#define PRISMDB_CASE(K)                                                  \
+  case K:                                                                \
+    if (verify) crc32c_fixed_kernel<K, true><<<grid, kThreads, 0, s>>>(a); \
+    else crc32c_fixed_kernel<K, false><<<grid, kThreads, 0, s>>>(a);       \
     break;
     PRISMDB_CASE(1) PRISMDB_CASE(2) PRISMDB_CASE(3) PRISMDB_CASE(4)
     PRISMDB_CASE(5) PRISMDB_CASE(6) PRISMDB_CASE(7) PRISMDB_CASE(8)

@@ -228,6 +228,44 @@ def test_verify_fixed_mode(dev, oracle):
     assert np.nonzero(mm.cpu().numpy())[0].tolist() == [17]
 
 
+@pytest.mark.parametrize("stride,length,nblk", [(3992, 3988, 4096), (4096, 4092, 4096), (256, 252, 20000),
+                                                (260, 256, 5000), (12, 8, 50000), (8, 4, 9000),
+                                                (4096, 2048, 3000), (4100, 1000, 7000), (4096, 4092, (1 << 20) + 77)])
+def test_verify_fixed_geometries(dev, oracle, stride, length, nblk, kernel_path):
+    """ReadBlock verify over fixed-stride spans on both kernels: clean
+    trailers, a flipped data byte, a flipped trailer byte, first/last spans
+    damaged; non-zero init against the oracle's verify; CRC output too."""
+    import torch
+    from prismdb_amd import crc32c
+
+    host = oracle.synth(nblk * stride + 8, 0x5EED0010 + length)
+    off = np.arange(nblk, dtype=np.uint64) * stride
+    lens = np.full(nblk, length, dtype=np.uint32)
+    want, _ = oracle.batch(host, off, lens)
+    tr = (((want >> 15) | (want << 17)) + np.uint32(0xA282EAD8)).astype("<u4").view(np.uint8).reshape(-1, 4)
+    idx = (off.astype(np.int64)[:, None] + length + np.arange(4)[None, :]).reshape(-1)
+    host[idx] = tr.reshape(-1)
+    bad = sorted({0, nblk // 3, nblk // 2, nblk - 1})
+    host[int(off[nblk // 3]) + length // 2] ^= 0x20          # data byte
+    host[int(off[nblk // 2]) + length + 3] ^= 0x01           # trailer byte
+    host[int(off[0])] ^= 0x80
+    host[int(off[nblk - 1]) + length - 1] ^= 0x02
+    buf = _to_dev(host, dev)
+    out, mm = crc32c.batch_fixed(buf, stride, length, nblk, verify=True)
+    torch.cuda.synchronize()
+    assert np.nonzero(mm.cpu().numpy())[0].tolist() == bad
+    want2, wmm = oracle.batch(host, off, lens, verify=True)
+    np.testing.assert_array_equal(_u32(out), want2)
+    np.testing.assert_array_equal(mm.cpu().numpy(), wmm)
+    init = 0x31415926
+    out3, mm3 = crc32c.batch_fixed(buf, stride, length, nblk, init=init, verify=True)
+    want3, wmm3 = oracle.batch(host, off, lens, np.full(nblk, init, dtype=np.uint32), verify=True)
+    np.testing.assert_array_equal(_u32(out3), want3)
+    np.testing.assert_array_equal(mm3.cpu().numpy(), wmm3)
+    del buf
+    torch.cuda.empty_cache()
+
+
 def test_full_size_config2_properties(dev, oracle):
     """BASELINE config 2 at full size (16 Mi x 4 KiB = 64 GiB): fixed-stride and
     descriptor paths agree on every block; 4096 sampled blocks (and the first
