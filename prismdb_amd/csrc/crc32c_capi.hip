@@ -15,6 +15,10 @@
 
 #include "../../include/prismdb_crc32c.h"
 #include "crc32c_device.h"
+
+#ifndef PRISMDB_SPAN_J0
+#define PRISMDB_SPAN_J0 0
+#endif
 #include "crc32c_gf2.h"
 
 namespace {
@@ -146,8 +150,10 @@ void InitDevice(DeviceCtx& ctx, int device) {
     ctx.error = t_last_error;
     return;
   }
+#if PRISMDB_SPAN_J0 == 0  // measurement-only builds compute wrong CRCs on purpose
   ctx.status = SelfTest(ctx);
   if (ctx.status != 0) ctx.error = t_last_error;
+#endif
 }
 
 int GetCtx(DeviceCtx** out) {
@@ -163,26 +169,33 @@ int GetCtx(DeviceCtx** out) {
 }
 
 // ---- generic-path workspace, per (thread, device, stream) ----
-// Fixed part: split-path counters, segment records/results, long-span list.
-// Growing part: one 16-byte record per span of the largest batch seen (the
-// first call with a larger batch synchronises the stream and reallocates).
+// Fixed part: split-path counters, segment records/results, long-span list,
+// planner block sums.  Growing part, sized for the largest batch seen (the
+// first call with a larger batch synchronises the stream and reallocates): per
+// span a 16-byte record and a 4-byte task count, plus the slice starts.
 struct Workspace {
   void* mem = nullptr;
-  prismdb::dev::SpanRec* rec = nullptr;
+  char* grow = nullptr;
   size_t cap_rec = 0;
   SplitWs ws{};
 };
 
+// Slice starts needed for n spans: nslices + 1 <= n/2 + 32 * streams + 2
+// (crc32c_slice_scan_kernel: tau = 64 gives <= n/2 + 1 slices of <= 32-task
+// spans; a smaller tau keeps tau > T / (32 * streams)).
+size_t SliceCap(size_t n, uint32_t streams) { return n / 2 + 32 * (size_t)streams + 4; }
+
 constexpr uint64_t kCapSeg = 1u << 20;   // 1 Mi segments = 32 GiB of long spans per call
 constexpr uint32_t kCapLong = 1u << 18;
 
-int GetWorkspace(hipStream_t s, size_t nspans, SplitWs* out) {
+int GetWorkspace(hipStream_t s, size_t nspans, uint32_t streams, SplitWs* out) {
   thread_local std::map<std::pair<int, hipStream_t>, Workspace> cache;
   int device = 0;
   hipGetDevice(&device);
   Workspace& w = cache[{device, s}];
   if (w.mem == nullptr) {
-    const size_t bytes = 256 + kCapSeg * (16 + 4) + (size_t)kCapLong * (8 + 8 + 4);
+    const size_t bytes = 256 + kCapSeg * (16 + 4) + (size_t)kCapLong * (8 + 8 + 4) +
+                         (size_t)prismdb::dev::kMaxPlanBlocks * 8;
     hipError_t e = hipMalloc(&w.mem, bytes);
     if (e != hipSuccess) {
       w.mem = nullptr;
@@ -200,22 +213,33 @@ int GetWorkspace(hipStream_t s, size_t nspans, SplitWs* out) {
     w.ws.seg_out = reinterpret_cast<uint32_t*>(p);
     p += kCapSeg * 4;
     w.ws.long_nseg = reinterpret_cast<uint32_t*>(p);
+    p += (size_t)kCapLong * 4;
+    w.ws.bsum = reinterpret_cast<uint64_t*>(p);
     w.ws.cap_seg = kCapSeg;
     w.ws.cap_long = kCapLong;
   }
   if (w.cap_rec < nspans) {
-    if (w.rec != nullptr) {
+    if (w.grow != nullptr) {
       hipStreamSynchronize(s);  // earlier batches on this stream may still read it
-      hipFree(w.rec);
-      w.rec = nullptr;
+      hipFree(w.grow);
+      w.grow = nullptr;
       w.cap_rec = 0;
     }
     const size_t cap = nspans < 4096 ? 4096 : nspans + nspans / 4;
-    hipError_t e = hipMalloc(reinterpret_cast<void**>(&w.rec), cap * 16);
+    const size_t bytes = cap * (16 + 4) + SliceCap(cap, streams) * 8 + 16;
+    hipError_t e = hipMalloc(reinterpret_cast<void**>(&w.grow), bytes);
     if (e != hipSuccess) return FailHip(e, "span record workspace hipMalloc");
     w.cap_rec = cap;
   }
-  w.ws.rec = w.rec;
+  w.ws.rec = reinterpret_cast<prismdb::dev::SpanRec*>(w.grow);
+  w.ws.slice_start = reinterpret_cast<uint64_t*>(w.grow + w.cap_rec * 16);
+  w.ws.cnt = reinterpret_cast<uint32_t*>(w.grow + w.cap_rec * 16 + SliceCap(w.cap_rec, streams) * 8);
+  // Planner tiles: whole multiples of its block size, at most kMaxPlanBlocks.
+  namespace d = prismdb::dev;
+  const uint64_t per = (nspans + d::kMaxPlanBlocks - 1) / d::kMaxPlanBlocks;
+  w.ws.tile = (per + d::kPlanThreads - 1) / d::kPlanThreads * d::kPlanThreads;
+  w.ws.nblocks = (uint32_t)((nspans + w.ws.tile - 1) / w.ws.tile);
+  w.ws.nstreams = streams;
   *out = w.ws;
   return 0;
 }
@@ -238,8 +262,29 @@ int RunBatch(DeviceCtx& ctx, const SpanBatch& base_args, bool desc, bool verify,
     hipError_t e = prismdb::dev::launch_fixed(a, verify, ctx.cus, s);
     return e == hipSuccess ? 0 : FailHip(e, "fixed kernel launch");
   }
+  // The span kernel indexes records with 32 bits: cut larger batches.
+  if (a.n > prismdb::dev::kMaxGenericSpans) {
+    for (uint64_t i = 0; i < a.n; i += prismdb::dev::kMaxGenericSpans) {
+      SpanBatch p = base_args;
+      p.n = a.n - i < prismdb::dev::kMaxGenericSpans ? a.n - i : prismdb::dev::kMaxGenericSpans;
+      if (desc) {
+        p.off += i;
+        p.len += i;
+        if (p.init != nullptr) p.init += i;
+      } else {
+        p.base += i * a.stride;
+      }
+      if (p.out != nullptr) p.out += i;
+      if (p.mismatch != nullptr) p.mismatch += i;
+      const int rc = RunBatch(ctx, p, desc, verify, s);
+      if (rc != 0) return rc;
+    }
+    return 0;
+  }
   SplitWs ws{};
-  int rc = GetWorkspace(s, a.n, &ws);
+  // The span kernel's record streams: two per wave of its persistent grid.
+  const uint32_t streams = 2u * (uint32_t)ctx.cus * prismdb::dev::kWavesPerGroup;
+  int rc = GetWorkspace(s, a.n, streams, &ws);
   if (rc != 0) return rc;
   hipError_t e = hipMemsetAsync(ws.counters, 0, sizeof(SplitCounters), s);
   if (e != hipSuccess) return FailHip(e, "hipMemsetAsync");
@@ -248,6 +293,10 @@ int RunBatch(DeviceCtx& ctx, const SpanBatch& base_args, bool desc, bool verify,
   a.rec = ws.rec;
   e = prismdb::dev::launch_plan(a, desc, ws, s);
   if (e != hipSuccess) return FailHip(e, "plan kernel launch");
+  e = prismdb::dev::launch_slices(a, ws, s);
+  if (e != hipSuccess) return FailHip(e, "slice kernels launch");
+  a.slice_start = ws.slice_start;
+  a.nslices_dev = &ws.counters->nslices;
   e = prismdb::dev::launch_span(a, verify, ctx.cus, s);
   if (e != hipSuccess) return FailHip(e, "span kernel launch");
   SpanBatch seg{};

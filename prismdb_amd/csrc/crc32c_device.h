@@ -59,12 +59,20 @@ struct SpanBatch {
   uint32_t role;
   const DeviceTables* tabs;
   const SpanRec* rec;               // span records (generic kernel)
+  // Task-balanced schedule (span role): slice k is records
+  // [slice_start[k], slice_start[k+1]), *nslices_dev slices; nullable: slices
+  // are runs of equal record counts instead (segment role).
+  const uint64_t* slice_start;
+  const unsigned long long* nslices_dev;
 };
 
 struct SplitCounters {
   unsigned long long nseg;
   uint32_t nlong;
   uint32_t overflow;
+  unsigned long long tasks;    // chunk tasks of the span pass (long spans count 1)
+  unsigned long long nslices;  // slices of 2^lg_tau tasks
+  uint32_t lg_tau;
 };
 
 struct SplitWs {
@@ -77,11 +85,23 @@ struct SplitWs {
   uint32_t* long_nseg;
   uint64_t cap_seg;
   uint32_t cap_long;
+  // task-balanced slices of the span pass
+  uint32_t* cnt;          // tasks of each span
+  uint64_t* bsum;         // per planner block: task sum, then its exclusive prefix
+  uint64_t* slice_start;  // nslices + 1 entries
+  uint64_t tile;          // records per planner block
+  uint32_t nblocks;       // planner blocks (<= kMaxPlanBlocks)
+  uint32_t nstreams;      // span-kernel record streams (2 per wave)
 };
+
+constexpr uint32_t kMaxPlanBlocks = 4096;
+constexpr uint64_t kMaxGenericSpans = 1ull << 30;  // per generic-path launch sequence
+constexpr uint32_t kPlanThreads = 256;
 
 hipError_t launch_span(const SpanBatch& a, bool verify, int grid, hipStream_t s);
 hipError_t launch_fixed(const SpanBatch& a, bool verify, int grid, hipStream_t s);
 hipError_t launch_plan(const SpanBatch& a, bool desc, const SplitWs& ws, hipStream_t s);
+hipError_t launch_slices(const SpanBatch& a, const SplitWs& ws, hipStream_t s);
 hipError_t launch_combine(const SpanBatch& a, bool desc, bool verify, const SplitWs& ws,
                           hipStream_t s);
 

@@ -29,6 +29,7 @@
 //                           verify: the stored trailer word rides in round 0
 //   crc32c_plan_kernel      one thread per span: 16-byte span records (all
 //                           geometry precomputed), long spans cut into segments
+//   crc32c_slice_{scan,mark}_kernel  task-balanced slices of the span records
 //   crc32c_span_kernel      everything else, driven by the span records
 //   crc32c_combine_kernel   stitches segments back into long spans
 #include <hip/hip_runtime.h>
@@ -50,6 +51,9 @@
 #endif
 #ifndef PRISMDB_XOR3
 #define PRISMDB_XOR3 1  // three-input XORs through v_bitop3_b32
+#endif
+#ifndef PRISMDB_SPAN_J0  // measurement knob: span kernel folds rounds >= this only (wrong results)
+#define PRISMDB_SPAN_J0 0
 #endif
 #ifndef PRISMDB_RUN_LG
 #define PRISMDB_RUN_LG 5  // fixed kernel: log2(pair steps per run); runs of 2 << PRISMDB_RUN_LG spans
@@ -334,12 +338,17 @@ __device__ __forceinline__ SpanRec make_rec(const uint8_t* p, uint32_t len, uint
   return r;
 }
 
-// Wave-uniform task: chunk c of the span with record r at index b.
+// Wave-uniform task: chunk c of the span with record r at index b, which is
+// record `slot` of its slice (`last`: the slice's final record).
 struct Task {
-  uint64_t b;
+  uint32_t b;
   SpanRec r;
   uint32_t c;
-  bool valid, skip;
+  uint32_t f;  // slot | last << 8 | valid << 9 | skip << 10: one SGPR, not four
+  __device__ uint32_t slot() const { return f & 255u; }
+  __device__ bool last() const { return (f >> 8) & 1u; }
+  __device__ bool valid() const { return (f >> 9) & 1u; }
+  __device__ bool skip() const { return (f >> 10) & 1u; }
   __device__ const uint8_t* body() const {
     return reinterpret_cast<const uint8_t*>(((uint64_t)(r.y & 0xffffu) << 32) | r.x);
   }
@@ -364,10 +373,11 @@ struct Task {
 // ---------------------------------------------------------------------------
 template <bool kVerify>
 __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
-  uint64_t n = a.n;
+  // Record indices are 32-bit: the host cuts generic batches at kMaxGenericSpans.
+  uint32_t n = (uint32_t)a.n;
   if (a.n_dev != nullptr) {
     const uint64_t m = *a.n_dev;
-    n = m < n ? m : n;
+    n = m < n ? (uint32_t)m : n;
   }
   const bool hdr = (a.flags & kFlagLogHeader) != 0;
   bool skip_long = a.role == kRoleSpans;  // long spans go through segments...
@@ -385,51 +395,86 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
   const StrideLanes tab = stride_lanes(lane);
   const uint32_t nibtab = 4u * (kTabWords + lane);  // byte address of lane's nibble entry [0][0]
   const ShortShift ss = short_shift_cols(lane);
-  const uint64_t wave = rfl(blockIdx.x * kWavesPerGroup + (tid >> 6));
-  const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerGroup;
-  // Spans are dealt in runs of kRun consecutive records per stream: run r of
-  // stream s of wave w is records [((r * nwaves + w) * 2 + s) * kRun, +kRun).
-  // Lane i of res[s] / bad[s] collects the run's i-th result / verify flag,
-  // stored with one coalesced nt store per run (scattered 4-byte stores cost
-  // 10 % of the read rate; the fixed kernel's comment has the measurement).
-  // kRun = 64, shortened so every stream gets >= 16 runs: with spans of mixed
-  // sizes, fewer and longer runs leave the last ones unbalanced (config 3 and
-  // the adversarial mix lost 4 % at >= 4 runs), and long spans make the
-  // per-span store a small share anyway.
+  const uint32_t wave = rfl(blockIdx.x * kWavesPerGroup + (tid >> 6));
+  const uint32_t nwaves = gridDim.x * kWavesPerGroup;
+  // Schedule.  The records are cut into slices of consecutive records, and
+  // the wave's stream s (of S = 2 * nwaves) takes slices s, s + S, s + 2S, ...
+  // so all streams sweep the batch front to back together.  Span role: slices
+  // of 2^lg_tau chunk tasks each (crc32c_slice_kernel), so every stream gets the
+  // same work whatever the span sizes and both streams of a wave run out
+  // together (dealing equal record counts left config 3's streams up to 30 %
+  // apart).  Segment role: slices of kRun records (segments are all but
+  // uniform), kRun = 64 shortened so every stream gets >= 16 slices.  A slice
+  // holds at most 64 records: lane i of res[s] / bad[s] collects its i-th
+  // result / verify flag, stored with one coalesced nt store when the slice's
+  // last record retires (scattered 4-byte stores cost 10 % of the read rate;
+  // the fixed kernel's comment has the measurement).
+  const uint32_t S = 2 * nwaves;
+  const bool sliced = a.slice_start != nullptr;
   uint32_t lg = 6;
-  while (lg > 0 && (n >> (lg + 1)) < nwaves * 16u) --lg;
-  const uint64_t kRun = 1ull << lg;
-  if ((wave << (lg + 1)) >= n) return;
-  auto next_rec = [&](uint64_t k) -> uint64_t {  // the stream's record after k
-    return ((k + 1) & (kRun - 1)) ? k + 1 : k + 1 + (2 * nwaves - 1) * kRun;
+  uint32_t K;
+  if (sliced) {
+    K = (uint32_t)const_load(a.nslices_dev, 0);  // <= n/2 + 32 S + 2
+  } else {
+    while (lg > 0 && (n >> (lg + 1)) < nwaves * 16u) --lg;
+    K = (uint32_t)(((uint64_t)n + (1u << lg) - 1) >> lg);
+  }
+  // Per stream: the pending record b (the one after the stream's newest task)
+  // and its slice k = [lo, hi); b = n once the stream has no records left.
+  struct Cursor {
+    uint32_t b, lo, hi, k;
+  };
+  auto open = [&](Cursor& c, uint32_t k) {  // first non-empty slice >= k of the stream
+    for (; k < K; k += S) {
+      uint32_t lo, hi;
+      if (sliced) {
+        lo = (uint32_t)const_load(a.slice_start, k);
+        hi = (uint32_t)const_load(a.slice_start, k + 1);
+      } else {
+        lo = k << lg;
+        hi = (uint32_t)((uint64_t)lo + (1u << lg) < n ? lo + (1u << lg) : n);
+      }
+      hi = hi < n ? hi : n;
+      if (lo < hi) {
+        c.b = c.lo = lo;
+        c.hi = hi;
+        c.k = k;
+        return;
+      }
+    }
+    c.b = c.lo = c.hi = n;
+    c.k = K;
+  };
+  auto advance = [&](Cursor& c) {
+    if (c.b + 1 < c.hi) ++c.b;
+    else open(c, c.k + S);
   };
 
-  auto read_rec = [&](uint64_t b) -> SpanRec {
+  auto read_rec = [&](uint32_t b) -> SpanRec {
     SpanRec r{0u, 0u, 0u, 0u};
     if (b < n) r = const_load(a.rec, b);
     return r;
   };
-  auto make_task = [&](uint64_t b, const SpanRec& r) -> Task {
+  auto make_task = [&](const Cursor& c, const SpanRec& r) -> Task {
     Task t;
-    t.b = b;
+    t.b = c.b;
     t.r = r;
     t.c = 0;
-    t.valid = b < n;
-    t.skip = !t.valid || (skip_long && t.lng());
+    const bool valid = c.b < n;
+    const bool skip = !valid || (skip_long && t.lng());
+    t.f = (c.b - c.lo) | (c.b + 1 == c.hi ? 1u << 8 : 0u) | (valid ? 1u << 9 : 0u) | (skip ? 1u << 10 : 0u);
     return t;
   };
-  SpanRec pend[2];  // record of the span after each stream's newest task
-  uint64_t pend_b[2];
+  Cursor cur[2];
+  SpanRec pend[2];  // record of each stream's pending record
   bool refill[2] = {false, false};
   auto next_task = [&](int s, const Task& t) -> Task {
-    if (t.c + 1 < t.nch()) {
+    if (!t.skip() && t.c + 1 < t.nch()) {  // a skipped (long) span is one task
       Task u = t;
       u.c = t.c + 1;
       return u;
     }
-    Task u = make_task(pend_b[s], pend[s]);
-    u.valid = u.valid && t.valid;
-    u.skip = u.skip || !u.valid;
+    Task u = make_task(cur[s], pend[s]);
     refill[s] = true;
     return u;
   };
@@ -438,14 +483,14 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
     for (int s = 0; s < 2; ++s) {
       if (refill[s]) {
         refill[s] = false;
-        pend_b[s] = next_rec(pend_b[s]);
-        pend[s] = read_rec(pend_b[s]);
+        advance(cur[s]);
+        pend[s] = read_rec(cur[s].b);
       }
     }
   };
   // 17 loads, always.
   auto issue = [&](const Task& t, uint32_t (&w)[kRounds], uint32_t& e) {
-    const bool live = !t.skip;
+    const bool live = !t.skip();
     const uint32_t pad = t.pad(), h = t.h(), tl = t.t(), nch = t.nch(), len = t.len();
     // Edge window: [start - hb, start + len + 4) when verifying a trailer after
     // the span, [start - 6, start + len) when the stored crc is a log header.
@@ -506,11 +551,11 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
       }
     }
   };
-  // Run results: flush lanes [0, kRun) of stream s's run starting at record base.
+  // Slice results: store lanes [0, t.slot()] of stream s's slice ending with task t.
   uint32_t res[2] = {0u, 0u}, bad[2] = {0u, 0u};
-  uint64_t unflushed[2] = {~0ull, ~0ull};  // base record of a run holding unstored results
-  auto flush = [&](int s, uint64_t base) {
-    if (lane < kRun && base + lane < n) {
+  auto flush = [&](int s, const Task& t) {
+    const uint32_t base = t.b - t.slot();
+    if (lane <= t.slot()) {
       if (a.out != nullptr) __builtin_nontemporal_store(res[s], a.out + base + lane);
       if (kVerify && a.mismatch != nullptr) __builtin_nontemporal_store((uint8_t)bad[s], a.mismatch + base + lane);
     }
@@ -521,7 +566,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
     const uint32_t d = tl ? readlane(e, 3) | (readlane(e, 4) << 8) | (readlane(e, 5) << 16) : 0u;
     const uint32_t crc = feed_short(ss, lane, t.r.z ? body : r[s], d, tl) ^ kConditioning;
     const uint32_t v = (a.flags & kFlagMask) ? mask_crc(crc) : crc;
-    const uint32_t slot = (uint32_t)(t.b & (kRun - 1));
+    const uint32_t slot = t.slot();
     res[s] = lane == slot ? v : res[s];
     if (kVerify) {
       const uint32_t stored = readlane(e, 6) | (readlane(e, 7) << 8) | (readlane(e, 8) << 16) | (readlane(e, 9) << 24);
@@ -529,26 +574,22 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
     }
     if ((a.flags & kFlagWriteTrailer) && lane == 0)
       store_le32(hdr ? t.start() - kLogCrcBack : t.body() + t.r.z + tl, v);
-    unflushed[s] = t.b - slot;
-    if (slot == kRun - 1) {
-      flush(s, t.b - slot);
-      unflushed[s] = ~0ull;
-    }
+    if (t.last()) flush(s, t);
   };
   // Fold the pair (stream 0 task tx in wx, stream 1 task ty in wy).
   auto fold = [&](const Task& tx, uint32_t (&wx)[kRounds], uint32_t ex, const Task& ty,
                   uint32_t (&wy)[kRounds], uint32_t ey) {
-    if (!tx.skip) begin(0, tx, wx, ex);
-    if (!ty.skip) begin(1, ty, wy, ey);
+    if (!tx.skip()) begin(0, tx, wx, ex);
+    if (!ty.skip()) begin(1, ty, wy, ey);
     uint32_t ax = acc[0], ay = acc[1];
 #pragma unroll
-    for (int j = 0; j < kRounds; ++j) {
+    for (int j = PRISMDB_SPAN_J0; j < kRounds; ++j) {
       ax = step256(lds, tab, ax, wx[j]);
       ay = step256(lds, tab, ay, wy[j]);
     }
     acc[0] = ax;
     acc[1] = ay;
-    const bool endx = !tx.skip && tx.c + 1 == tx.nch(), endy = !ty.skip && ty.c + 1 == ty.nch();
+    const bool endx = !tx.skip() && tx.c + 1 == tx.nch(), endy = !ty.skip() && ty.c + 1 == ty.nch();
     if (endx && endy) {
       const uint32_t vx = realign(lds, nibtab, ax), vy = realign(lds, nibtab, ay);
       const uint32_t bx = wave_xor(vx), by = wave_xor(vy);
@@ -559,6 +600,10 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
     } else if (endy) {
       finish(1, ty, ey, wave_xor(realign(lds, nibtab, ay)));
     }
+    // A skipped long span's result comes from the combine pass, but it may
+    // close its slice: the slice's other results are stored now.
+    if (tx.skip() && tx.valid() && tx.last()) flush(0, tx);
+    if (ty.skip() && ty.valid() && ty.last()) flush(1, ty);
   };
 
   // Ring: two slots x two streams, compile-time slot indices (loop unrolled
@@ -570,11 +615,12 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
   uint32_t eb[2][2];
 #pragma unroll
   for (int st = 0; st < 2; ++st) {
-    const uint64_t b0 = (2 * wave + st) * kRun;
-    tk[0][st] = make_task(b0, read_rec(b0));
-    pend_b[st] = next_rec(b0);
-    pend[st] = read_rec(pend_b[st]);
+    open(cur[st], 2 * wave + st);
+    tk[0][st] = make_task(cur[st], read_rec(cur[st].b));
+    advance(cur[st]);
+    pend[st] = read_rec(cur[st].b);
   }
+  if (!tk[0][0].valid() && !tk[0][1].valid()) return;
   tk[1][0] = next_task(0, tk[0][0]);
   tk[1][1] = next_task(1, tk[0][1]);
   refill_recs();
@@ -590,7 +636,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
       wait_task<kYounger>(wb[sl][0], eb[sl][0]);
       wait_task<kYounger>(wb[sl][1], eb[sl][1]);
       fold(tk[sl][0], wb[sl][0], eb[sl][0], tk[sl][1], wb[sl][1], eb[sl][1]);
-      if (!tk[sl ^ 1][0].valid && !tk[sl ^ 1][1].valid) goto drained;
+      if (!tk[sl ^ 1][0].valid() && !tk[sl ^ 1][1].valid()) goto drained;
       tk[sl][0] = next_task(0, tk[sl ^ 1][0]);
       tk[sl][1] = next_task(1, tk[sl ^ 1][1]);
       refill_recs();
@@ -600,16 +646,12 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
   }
 drained:
   // Retire the abandoned slot's loads while their registers are live (see the
-  // fixed kernel's drain), then store the partial last runs: every record < n
-  // of them is done.
+  // fixed kernel's drain).  Every slice was stored when its last record retired.
 #pragma unroll
   for (int sl = 0; sl < 2; ++sl) {
     wait_task<0>(wb[sl][0], eb[sl][0]);
     wait_task<0>(wb[sl][1], eb[sl][1]);
   }
-#pragma unroll
-  for (int st = 0; st < 2; ++st)
-    if (unflushed[st] != ~0ull) flush(st, unflushed[st]);
 }
 
 // ---------------------------------------------------------------------------
@@ -771,23 +813,33 @@ __global__ __launch_bounds__(kThreads) void crc32c_fixed_kernel(SpanBatch a) {
 }
 
 // ---------------------------------------------------------------------------
-// Planner: one thread per span writes its record; spans longer than
-// skip_above become segments [first piece of len - (nseg-1)*kSegment bytes
-// with the span's init] + nseg-1 pieces of kSegment bytes with init
+// Planner: one thread per span writes its record and its task count; spans
+// longer than skip_above become segments [first piece of len - (nseg-1)*kSegment
+// bytes with the span's init] + nseg-1 pieces of kSegment bytes with init
 // 0xFFFFFFFF (Extend(~0, d) ^ ~0 is the raw register R(0, d)), each with its
-// own record for the segment pass.
+// own record for the segment pass.  Block b covers records [b*tile, +tile) and
+// leaves its task sum in bsum[b] for the slice scan.
 // ---------------------------------------------------------------------------
 template <bool kDesc>
-__global__ __launch_bounds__(256) void crc32c_plan_kernel(SpanBatch a, SplitWs ws) {
+__global__ __launch_bounds__(kPlanThreads) void crc32c_plan_kernel(SpanBatch a, SplitWs ws) {
   const uint64_t n = a.n;
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-       i += (uint64_t)gridDim.x * blockDim.x) {
+  const uint64_t lo = (uint64_t)blockIdx.x * ws.tile;
+  const uint64_t hi = lo + ws.tile < n ? lo + ws.tile : n;
+  __shared__ unsigned long long sum;
+  if (threadIdx.x == 0) sum = 0;
+  __syncthreads();
+  uint32_t mine = 0;  // <= tile/256 spans of <= 32 tasks each
+  for (uint64_t i = lo + threadIdx.x; i < hi; i += kPlanThreads) {
     const uint64_t off = kDesc ? a.off[i] : i * a.stride;
     const uint32_t len = kDesc ? a.len[i] : a.len_c;
     const uint32_t init = kDesc ? (a.init != nullptr ? a.init[i] : 0u) : a.init_c;
     const uint8_t* p = a.base + off;
     const bool lng = len > a.skip_above;
-    ws.rec[i] = make_rec(p, len, init, lng);
+    const SpanRec r = make_rec(p, len, init, lng);
+    ws.rec[i] = r;
+    const uint32_t cnt = lng ? 1u : (r.z ? (r.z + 4095u) >> 12 : 1u);  // Task::nch()
+    ws.cnt[i] = cnt;
+    mine += cnt;
     if (!lng) continue;
     const uint32_t nseg = (len + kSegment - 1u) / kSegment;
     const uint32_t first = len - (nseg - 1u) * kSegment;
@@ -803,6 +855,89 @@ __global__ __launch_bounds__(256) void crc32c_plan_kernel(SpanBatch a, SplitWs w
     ws.seg_rec[pos] = make_rec(p, first, init, false);
     for (uint32_t s = 1; s < nseg; ++s)
       ws.seg_rec[pos + s] = make_rec(p + first + (uint64_t)(s - 1u) * kSegment, kSegment, kConditioning, false);
+  }
+  atomicAdd(&sum, (unsigned long long)mine);
+  __syncthreads();
+  if (threadIdx.x == 0) ws.bsum[blockIdx.x] = sum;
+}
+
+// Exclusive prefix of v over the block's kPlanThreads threads (LDS, log steps).
+__device__ uint64_t block_exclusive_scan(uint64_t v, uint64_t* sh, uint64_t& total) {
+  const uint32_t t = threadIdx.x;
+  sh[t] = v;
+  __syncthreads();
+  for (uint32_t d = 1; d < blockDim.x; d <<= 1) {
+    const uint64_t x = t >= d ? sh[t - d] : 0u;
+    __syncthreads();
+    sh[t] += x;
+    __syncthreads();
+  }
+  const uint64_t incl = sh[t];
+  total = sh[blockDim.x - 1];
+  __syncthreads();
+  return incl - v;
+}
+
+// ---------------------------------------------------------------------------
+// Slice schedule of the span pass.  T tasks in all; slices of tau = 2^lg_tau
+// tasks, tau = 64 or smaller so that each of the span kernel's S streams gets
+// >= 16 slices; slice k = the records whose first task falls in
+// [k*tau, (k+1)*tau), so a slice holds <= tau <= 64 records (every record is
+// >= 1 task) and slice_start[k] = first record whose first task is >= k*tau.
+//   scan kernel (1 block): exclusive prefix of the planner blocks' sums, T,
+//                          lg_tau, nslices, slice_start[0] and [nslices]
+//   mark kernel (planner tiles): record i with first task E and c tasks opens
+//                          slices (E/tau, (E+c)/tau]: slice_start[k] = i + 1
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(1024) void crc32c_slice_scan_kernel(SpanBatch a, SplitWs ws) {
+  __shared__ uint64_t sh[1024];
+  const uint32_t t = threadIdx.x;
+  constexpr uint32_t kPer = kMaxPlanBlocks / 1024;
+  uint64_t v[kPer], mine = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < kPer; ++j) {
+    const uint32_t b = t * kPer + j;
+    v[j] = b < ws.nblocks ? ws.bsum[b] : 0u;
+    mine += v[j];
+  }
+  uint64_t T = 0;
+  uint64_t run = block_exclusive_scan(mine, sh, T);
+#pragma unroll
+  for (uint32_t j = 0; j < kPer; ++j) {
+    const uint32_t b = t * kPer + j;
+    if (b < ws.nblocks) ws.bsum[b] = run;
+    run += v[j];
+  }
+  if (t == 0) {
+    const uint64_t S = ws.nstreams;
+    uint32_t lg = 6;
+    while (lg > 0 && (T >> lg) < S * 16u) --lg;
+    const uint64_t K = (T + (1ull << lg) - 1) >> lg;
+    ws.counters->tasks = T;
+    ws.counters->lg_tau = lg;
+    ws.counters->nslices = K;
+    ws.slice_start[0] = 0;
+    ws.slice_start[K] = a.n;
+  }
+}
+
+__global__ __launch_bounds__(kPlanThreads) void crc32c_slice_mark_kernel(SpanBatch a, SplitWs ws) {
+  __shared__ uint64_t sh[kPlanThreads];
+  const uint64_t n = a.n;
+  const uint64_t lo = (uint64_t)blockIdx.x * ws.tile;
+  const uint64_t hi = lo + ws.tile < n ? lo + ws.tile : n;
+  const uint32_t lg = ws.counters->lg_tau;
+  const uint64_t K = ws.counters->nslices;
+  uint64_t base = ws.bsum[blockIdx.x];
+  for (uint64_t i0 = lo; i0 < hi; i0 += kPlanThreads) {  // uniform trip count: the scan syncs
+    const uint64_t i = i0 + threadIdx.x;
+    const uint32_t c = i < hi ? ws.cnt[i] : 0u;
+    uint64_t total = 0;
+    const uint64_t e = base + block_exclusive_scan(c, sh, total);
+    base += total;
+    if (i >= hi) continue;
+    const uint64_t k1 = (e + c) >> lg;
+    for (uint64_t k = (e >> lg) + 1; k <= k1 && k <= K; ++k) ws.slice_start[k] = i + 1;
   }
 }
 
@@ -870,10 +1005,14 @@ hipError_t launch_fixed(const SpanBatch& a, bool verify, int grid, hipStream_t s
 }
 
 hipError_t launch_plan(const SpanBatch& a, bool desc, const SplitWs& ws, hipStream_t s) {
-  const uint64_t want = (a.n + 255u) / 256u;
-  const int grid = (int)(want < 4096u ? (want ? want : 1u) : 4096u);
-  if (desc) crc32c_plan_kernel<true><<<grid, 256, 0, s>>>(a, ws);
-  else crc32c_plan_kernel<false><<<grid, 256, 0, s>>>(a, ws);
+  if (desc) crc32c_plan_kernel<true><<<ws.nblocks, kPlanThreads, 0, s>>>(a, ws);
+  else crc32c_plan_kernel<false><<<ws.nblocks, kPlanThreads, 0, s>>>(a, ws);
+  return hipGetLastError();
+}
+
+hipError_t launch_slices(const SpanBatch& a, const SplitWs& ws, hipStream_t s) {
+  crc32c_slice_scan_kernel<<<1, 1024, 0, s>>>(a, ws);
+  crc32c_slice_mark_kernel<<<ws.nblocks, kPlanThreads, 0, s>>>(a, ws);
   return hipGetLastError();
 }
 

@@ -185,6 +185,36 @@ def test_huge_span_split_path(dev, oracle):
     _check_spans(dev, oracle, host, [3, 17, (40 << 20) + 5], [40 << 20, 131073, 4000])
 
 
+def test_long_spans_close_slices(dev, oracle):
+    """300 000 short spans with long (split-path) spans at positions 63 mod 64
+    and elsewhere, plus 32-task spans: a slice whose last record is a skipped
+    long span must still store its other results (large batches, where a
+    slice holds up to 64 records)."""
+    rng = np.random.default_rng(0x5EED0011)
+    size = 48 << 20
+    host = oracle.synth(size, 0x5EED0011)
+    n = 300_000
+    lens = rng.integers(0, 300, size=n).astype(np.uint64)
+    idx_long = np.concatenate([np.arange(63, n, 64 * 37), rng.integers(0, n, size=200)])
+    lens[idx_long] = rng.integers(131073, 400_000, size=len(idx_long))
+    lens[rng.integers(0, n, size=500)] = 131072  # the longest span the span pass folds itself
+    off = rng.integers(0, size - 400_001, size=n).astype(np.uint64)
+    init = rng.integers(0, 2**32, size=n, dtype=np.uint64).astype(np.uint32)
+    _check_spans(dev, oracle, host, off, lens, init, mask=True)
+
+
+@pytest.mark.parametrize("n", [1, 7, 640, 5000])
+def test_slices_with_empty_slices(dev, oracle, n):
+    """Small batches of multi-task spans: the slice size drops to 1-2 tasks, so
+    a 32-task span opens many empty slices that streams must step over."""
+    rng = np.random.default_rng(0x5EED0012 + n)
+    size = 16 << 20
+    host = oracle.synth(size, 0x5EED0012)
+    lens = rng.choice([0, 1, 3, 4095, 4096, 4097, 65536, 131072, 200_000], size=n).astype(np.uint64)
+    off = rng.integers(0, size - 200_001, size=n).astype(np.uint64)
+    _check_spans(dev, oracle, host, off, lens)
+
+
 def test_verify_sst_fixture(dev, golden):
     """ReadBlock verify semantics on the reference-built SST, clean and corrupted."""
     import torch

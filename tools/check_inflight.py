@@ -13,7 +13,9 @@ fall-through) with a forward dataflow over "possibly in-flight" registers:
   * an asm load adds its destination registers at age 0;
   * `s_waitcnt vmcnt(N)` (asm or compiler) retires entries of age >= N;
   * ages are capped at 64 (vmcnt holds at most 63 outstanding operations);
-  * at a join the states are merged keeping each register's youngest age.
+  * at a join the states are merged keeping each register's youngest age;
+  * short branch-only blocks that test a constant SGPR pair / vcc are walked
+    per incoming edge, so a branch decided by a constant prunes its dead edge.
 
 Usage: check_inflight.py kernel.s   (the text of ONE kernel, e.g. cut with awk)
 Exit status 1 if any hazard is found.
@@ -128,30 +130,122 @@ def merge(a, b):
     return out
 
 
+SREG = re.compile(r"^s\[(\d+):(\d+)\]$|^s(\d+)$")
+
+
+def sregs(tok):
+    m = SREG.match(tok.strip())
+    if not m:
+        return {"vcc"} if tok.strip().startswith("vcc") else set()
+    if m.group(3) is not None:
+        return {int(m.group(3))}
+    return set(range(int(m.group(1)), int(m.group(2)) + 1))
+
+
+def cstep(consts, t):
+    """Constant SGPR-pair / vcc values through one instruction: enough to see
+    hipcc's loop-exit funnel (s_mov_b64 X, 0 ... s_xor_b64 X, X, -1;
+    s_andn2_b64 vcc, exec, X; s_cbranch_vccz) as the branch it always is."""
+    parts = t.split(None, 1)
+    op = parts[0]
+    ops = [o.strip() for o in parts[1].split(",")] if len(parts) > 1 else []
+    c = dict(consts)
+    if op == "s_mov_b64" and len(ops) == 2 and ops[1] in ("0", "-1"):
+        dst = ops[0]
+        c = {k: v for k, v in c.items() if not (sregs(k) & sregs(dst))}
+        c[dst] = int(ops[1])
+        return c
+    if op == "s_xor_b64" and len(ops) == 3 and ops[0] == ops[1] and ops[2] == "-1" and ops[0] in c:
+        c[ops[0]] = ~c[ops[0]]
+        return c
+    if op in ("s_andn2_b64", "s_and_b64") and len(ops) == 3 and ops[0] == "vcc" and ops[1] == "exec":
+        x = c.get(ops[2])
+        c.pop("vcc", None)
+        if x is not None:  # exec is non-zero in a running wave
+            zero = (x == -1) if op == "s_andn2_b64" else (x == 0)
+            c["vcc"] = 0 if zero else 1
+        return c
+    written = set()
+    if ops and (op.startswith("s_") or op.startswith("v_readlane") or op.startswith("v_readfirstlane")):
+        written = sregs(ops[0])
+    if op.startswith(("v_cmp", "v_add_co", "v_sub_co", "v_subrev_co", "v_addc", "v_subb", "v_div_scale")) or \
+            (ops and ops[0].startswith("vcc")):
+        written |= {"vcc"}
+    if written:
+        c = {k: v for k, v in c.items() if not (sregs(k) & written)}
+    return c
+
+
+def feasible(insts, bl, succ, n, consts):
+    """Successors of block n, dropping a vccz/vccnz edge that vcc rules out."""
+    a, b = bl[n]
+    t = insts[b - 1][1]
+    op = t.split()[0]
+    if op not in ("s_cbranch_vccz", "s_cbranch_vccnz") or "vcc" not in consts or len(succ[n]) != 2:
+        return succ[n]
+    taken = (consts["vcc"] == 0) == (op == "s_cbranch_vccz")
+    return [succ[n][0]] if taken else [succ[n][1]]
+
+
+def cmerge(a, b):
+    return {k: v for k, v in a.items() if b.get(k) == v}
+
+
 def main():
     insts, labels = parse(sys.argv[1])
     bl, succ = blocks(insts, labels)
     ins = [None] * len(bl)
+    cin = [None] * len(bl)
+
+    def is_threadable(n):
+        a, b = bl[n]
+        if b - a > 8 or insts[b - 1][1].split()[0] not in ("s_cbranch_vccz", "s_cbranch_vccnz"):
+            return False
+        return not any(insts[k][1].split()[0].startswith(VMEM) or insts[k][1].startswith("s_waitcnt")
+                       for k in range(a, b))
+
+    threadable = [n != 0 and is_threadable(n) for n in range(len(bl))]
     ins[0] = {}
+    cin[0] = {}
     work = [0]
     while work:
         n = work.pop()
         st = dict(ins[n])
+        cs = dict(cin[n])
         a, b = bl[n]
         for k in range(a, b):
             st = step(st, insts[k])
-        for s in succ[n]:
+            cs = cstep(cs, insts[k][1])
+        # Jump threading: a block with no vector-memory op or wait that ends in
+        # a vcc branch (the funnel) is walked per incoming edge, so a constant
+        # known on one edge is not lost in the merge with the others.
+        edges = [(s, cs) for s in feasible(insts, bl, succ, n, cs)]
+        hops = 0
+        while edges:
+            s, c = edges.pop()
+            if threadable[s] and hops < 64:
+                hops += 1
+                ins[s] = st if ins[s] is None else merge(ins[s], st)  # for the report pass
+                c2 = c
+                for k in range(bl[s][0], bl[s][1]):
+                    c2 = cstep(c2, insts[k][1])
+                edges.extend((t, c2) for t in feasible(insts, bl, succ, s, c2))
+                continue
             new = st if ins[s] is None else merge(ins[s], st)
-            if new != ins[s]:
+            newc = c if cin[s] is None else cmerge(cin[s], c)
+            if new != ins[s] or newc != cin[s]:
                 ins[s] = new
+                cin[s] = newc
                 work.append(s)
-    # The dataflow is path-insensitive: hipcc often funnels a loop exit through
-    # a flag-tested block that also falls into the loop header, which makes
-    # infeasible paths look like they carry young loads into the header.  So
-    # the verdict counts only the unambiguous pattern -- a read/copy of a
-    # possibly in-flight register placed BEFORE an asm vmcnt wait in the same
-    # basic block (the compiler materialising a ring register for the wait's
-    # "+v" operand from a stale copy) -- and reports the rest as "possible".
+    # Joins keep each register's youngest age.  hipcc funnels loop exits through
+    # a block that tests a constant-set SGPR pair (s_mov_b64 X, 0 ... s_xor_b64
+    # X, X, -1; s_andn2_b64 vcc, exec, X; s_cbranch_vccz) and also falls into
+    # the loop header; walking such blocks per incoming edge (jump threading
+    # above) drops those infeasible paths, which used to carry young loads into
+    # the header by the hundreds.  What is left is counted in two classes, and
+    # BOTH fail the audit: a touch placed before an asm vmcnt wait in its own
+    # block (the compiler materialising a ring register for the wait's "+v"
+    # operand from a stale copy), and any other touch.
     certain, possible = [], []
     for n, (a, b) in enumerate(bl):
         if ins[n] is None:
@@ -165,8 +259,10 @@ def main():
             (certain if k < last_wait else possible).extend(rep)
     for ln, t, regs in certain[:40]:
         print(f"line {ln}: {t}   in-flight {regs}  (before the asm wait of its block)")
-    print(f"{len(certain)} hazards; {len(possible)} possible on path-insensitive joins ({len(bl)} blocks)")
-    return 1 if certain else 0
+    for ln, t, regs in possible[:40]:
+        print(f"line {ln}: {t}   in-flight {regs}")
+    print(f"{len(certain)} hazards before a wait; {len(possible)} other hazards ({len(bl)} blocks)")
+    return 1 if certain or possible else 0
 
 
 if __name__ == "__main__":

@@ -26,6 +26,10 @@ VARIANTS = {
     "nofold_nt0": {"PRISMDB_FIXED_NOFOLD": 1, "PRISMDB_NT_LOADS": 0},
     "nostore": {"PRISMDB_FIXED_NOSTORE": 1},
     "nofold_nostore": {"PRISMDB_FIXED_NOFOLD": 1, "PRISMDB_FIXED_NOSTORE": 1},
+    # measurement-only: span kernel folds rounds >= 12 / none (wrong results): the
+    # ceiling of skipping chunk 0's padding rounds on ~1 KB spans
+    "span_j12": {"PRISMDB_SPAN_J0": 12},
+    "span_j16": {"PRISMDB_SPAN_J0": 16},
     # fixed kernel: runs of 16 spans per wave instead of 64
     "run3": {"PRISMDB_RUN_LG": 3},
 }
