@@ -402,20 +402,20 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
   // so all streams sweep the batch front to back together.  Span role: slices
   // of 2^lg_tau chunk tasks each (crc32c_slice_kernel), so every stream gets the
   // same work whatever the span sizes and both streams of a wave run out
-  // together (dealing equal record counts left config 3's streams up to 30 %
-  // apart).  Segment role: slices of kRun records (segments are all but
-  // uniform), kRun = 64 shortened so every stream gets >= 16 slices.  A slice
+  // together (dealt equal record counts, config 3's busiest stream had 26 %
+  // more tasks than the mean, and a wave folds its two streams in lockstep).  Segment role: slices of kRun records (segments are all but
+  // uniform; so are span-role batches whose spans are one task each), kRun =
+  // 64 shortened so every stream gets >= 16 slices.  A slice
   // holds at most 64 records: lane i of res[s] / bad[s] collects its i-th
   // result / verify flag, stored with one coalesced nt store when the slice's
   // last record retires (scattered 4-byte stores cost 10 % of the read rate;
   // the fixed kernel's comment has the measurement).
   const uint32_t S = 2 * nwaves;
-  const bool sliced = a.slice_start != nullptr;
+  bool sliced = a.slice_start != nullptr;
   uint32_t lg = 6;
-  uint32_t K;
-  if (sliced) {
-    K = (uint32_t)const_load(a.nslices_dev, 0);  // <= n/2 + 32 S + 2
-  } else {
+  uint32_t K = sliced ? (uint32_t)const_load(a.nslices_dev, 0) : 0u;  // <= n/2 + 32 S + 2; 0: runs
+  if (K == 0) {
+    sliced = false;
     while (lg > 0 && (n >> (lg + 1)) < nwaves * 16u) --lg;
     K = (uint32_t)(((uint64_t)n + (1u << lg) - 1) >> lg);
   }
@@ -915,29 +915,35 @@ __global__ __launch_bounds__(1024) void crc32c_slice_scan_kernel(SpanBatch a, Sp
     const uint64_t K = (T + (1ull << lg) - 1) >> lg;
     ws.counters->tasks = T;
     ws.counters->lg_tau = lg;
-    ws.counters->nslices = K;
+    // Every span one task (4 KiB blocks, log records, SST data blocks): slices
+    // of tau tasks are runs of tau records, which the span kernel deals
+    // without slice starts -- nslices = 0 says so and the mark pass is skipped.
+    ws.counters->nslices = T == a.n ? 0 : K;
     ws.slice_start[0] = 0;
     ws.slice_start[K] = a.n;
   }
 }
 
 __global__ __launch_bounds__(kPlanThreads) void crc32c_slice_mark_kernel(SpanBatch a, SplitWs ws) {
+  const uint64_t K = ws.counters->nslices;
+  if (K == 0) return;  // uniform batch: runs, no slice starts
   __shared__ uint64_t sh[kPlanThreads];
   const uint64_t n = a.n;
-  const uint64_t lo = (uint64_t)blockIdx.x * ws.tile;
-  const uint64_t hi = lo + ws.tile < n ? lo + ws.tile : n;
   const uint32_t lg = ws.counters->lg_tau;
-  const uint64_t K = ws.counters->nslices;
-  uint64_t base = ws.bsum[blockIdx.x];
-  for (uint64_t i0 = lo; i0 < hi; i0 += kPlanThreads) {  // uniform trip count: the scan syncs
-    const uint64_t i = i0 + threadIdx.x;
-    const uint32_t c = i < hi ? ws.cnt[i] : 0u;
-    uint64_t total = 0;
-    const uint64_t e = base + block_exclusive_scan(c, sh, total);
-    base += total;
-    if (i >= hi) continue;
+  // Thread t walks its own per = tile/256 consecutive records of the block's
+  // tile: one block scan per tile instead of one per 256 records.
+  const uint64_t per = ws.tile / kPlanThreads;
+  const uint64_t lo = (uint64_t)blockIdx.x * ws.tile + threadIdx.x * per;
+  const uint64_t hi = lo + per < n ? lo + per : n;
+  uint64_t mine = 0;
+  for (uint64_t i = lo; i < hi; ++i) mine += ws.cnt[i];
+  uint64_t total = 0;
+  uint64_t e = ws.bsum[blockIdx.x] + block_exclusive_scan(mine, sh, total);
+  for (uint64_t i = lo; i < hi; ++i) {
+    const uint32_t c = ws.cnt[i];
     const uint64_t k1 = (e + c) >> lg;
     for (uint64_t k = (e >> lg) + 1; k <= k1 && k <= K; ++k) ws.slice_start[k] = i + 1;
+    e += c;
   }
 }
 

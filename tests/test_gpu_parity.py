@@ -185,11 +185,13 @@ def test_huge_span_split_path(dev, oracle):
     _check_spans(dev, oracle, host, [3, 17, (40 << 20) + 5], [40 << 20, 131073, 4000])
 
 
-def test_long_spans_close_slices(dev, oracle):
+@pytest.mark.parametrize("uniform", [False, True])
+def test_long_spans_close_slices(dev, oracle, uniform):
     """300 000 short spans with long (split-path) spans at positions 63 mod 64
-    and elsewhere, plus 32-task spans: a slice whose last record is a skipped
-    long span must still store its other results (large batches, where a
-    slice holds up to 64 records)."""
+    and elsewhere: a slice whose last record is a skipped long span must still
+    store its other results (large batches, where a slice holds up to 64
+    records).  uniform: every span one task (runs of 64 records, no slice
+    starts); else 32-task spans too (task-balanced slices)."""
     rng = np.random.default_rng(0x5EED0011)
     size = 48 << 20
     host = oracle.synth(size, 0x5EED0011)
@@ -197,7 +199,8 @@ def test_long_spans_close_slices(dev, oracle):
     lens = rng.integers(0, 300, size=n).astype(np.uint64)
     idx_long = np.concatenate([np.arange(63, n, 64 * 37), rng.integers(0, n, size=200)])
     lens[idx_long] = rng.integers(131073, 400_000, size=len(idx_long))
-    lens[rng.integers(0, n, size=500)] = 131072  # the longest span the span pass folds itself
+    if not uniform:
+        lens[rng.integers(0, n, size=500)] = 131072  # the longest span the span pass folds itself
     off = rng.integers(0, size - 400_001, size=n).astype(np.uint64)
     init = rng.integers(0, 2**32, size=n, dtype=np.uint64).astype(np.uint32)
     _check_spans(dev, oracle, host, off, lens, init, mask=True)
