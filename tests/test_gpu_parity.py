@@ -206,6 +206,45 @@ def test_long_spans_close_slices(dev, oracle, uniform):
     _check_spans(dev, oracle, host, off, lens, init, mask=True)
 
 
+def test_log_header_padding_skip(dev, oracle):
+    """LOG_HEADER batches run the span kernel that skips chunk 0's padding
+    rounds: short records paired with multi-chunk ones, empty and 1-3 byte
+    records, random offsets; CRCs and the verify flags against the oracle
+    (the stored crc sits 6 bytes before each span, db/log_reader.cc:246-257)."""
+    import torch
+    from prismdb_amd import crc32c
+
+    rng = np.random.default_rng(0x5EED0013)
+    size = 32 << 20
+    host = oracle.synth(size, 0x5EED0013)
+    n = 20_000
+    lens = np.where(rng.random(n) < 0.8, rng.integers(0, 1100, size=n),
+                    rng.integers(1100, 40_000, size=n)).astype(np.uint64)
+    lens[:50] = np.arange(50)
+    off = rng.integers(6, size - 40_001, size=n).astype(np.uint64)
+    init = rng.integers(0, 2**32, size=n, dtype=np.uint64).astype(np.uint32)
+    want, _ = oracle.batch(host, off, lens, init)
+    # store the masked crc 6 bytes before half of the spans
+    good = rng.random(n) < 0.5
+    for i in np.nonzero(good)[0][:2000]:
+        o = int(off[i]) - 6
+        host[o:o + 4] = np.frombuffer(np.uint32(oracle.mask(int(want[i]))).tobytes(), dtype=np.uint8)
+    want, _ = oracle.batch(host, off, lens, init)  # stores may land inside other spans
+    stored = np.array([int.from_bytes(host[int(o) - 6:int(o) - 2].tobytes(), "little") for o in off], dtype=np.uint64)
+    want_bad = np.array([oracle.unmask(int(s)) != int(w) for s, w in zip(stored, want)], dtype=np.uint8)
+    buf = _to_dev(host, dev)
+    d_off = _to_dev(off.astype(np.int64), dev)
+    d_len = _to_dev(lens.astype(np.uint32).view(np.int32), dev)
+    d_init = _to_dev(init.view(np.int32), dev)
+    out, _ = crc32c.batch(buf, d_off, d_len, d_init, log_header=True)
+    np.testing.assert_array_equal(_u32(out), want)
+    out2, mm = crc32c.batch(buf, d_off, d_len, d_init, verify=True, log_header=True)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(_u32(out2), want)
+    np.testing.assert_array_equal(mm.cpu().numpy(), want_bad)
+    assert want_bad.sum() < n  # some stored crcs match
+
+
 @pytest.mark.parametrize("n", [1, 7, 640, 5000])
 def test_slices_with_empty_slices(dev, oracle, n):
     """Small batches of multi-task spans: the slice size drops to 1-2 tasks, so

@@ -1,0 +1,19 @@
+#!/bin/bash
+# two-path fold (straight when both chunks full): parity suite, A/B prev (aa4ceca) vs per-round skip vs two-path
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 900 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread > gpurun_out/ag_tests.log 2>&1 && \
+timeout -k 10 500 python tools/variants.py run --only prev skip1 base --gib 64 --reps 7 > gpurun_out/ag_variants.json 2>gpurun_out/ag_variants.err
+rc=$?
+tail -3 gpurun_out/ag_tests.log
+python - <<'PY'
+import json
+try:
+    d = json.load(open("gpurun_out/ag_variants.json"))
+    print(d["agree"])
+    for w, r in d["results"].items():
+        print(w, {n: v["GB/s_median"] for n, v in r.items()})
+except Exception as e:
+    print("variants:", e)
+PY
+exit $rc
