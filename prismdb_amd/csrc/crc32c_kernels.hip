@@ -55,6 +55,12 @@
 #ifndef PRISMDB_SPAN_J0  // measurement knob: span kernel folds rounds >= this only (wrong results)
 #define PRISMDB_SPAN_J0 0
 #endif
+#ifndef PRISMDB_SPAN_NOSWITCH  // measurement knob: initial register always enters round 0 (wrong if pad >= 64)
+#define PRISMDB_SPAN_NOSWITCH 0
+#endif
+#ifndef PRISMDB_SPAN_SNOP  // 1: s_nop 4 between the descriptors and the asm buffer loads
+#define PRISMDB_SPAN_SNOP 0
+#endif
 #ifndef PRISMDB_RUN_LG
 #define PRISMDB_RUN_LG 5  // fixed kernel: log2(pair steps per run); runs of 2 << PRISMDB_RUN_LG spans
 #endif
@@ -497,10 +503,17 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
     const uint32_t hb = kVerify && hdr ? kLogCrcBack : 0u;
     u32x4 rb = buffer_rsrc(t.body(), live ? t.r.z : 0u);
     u32x4 re = buffer_rsrc(t.start() - hb, live ? hb + len + (kVerify && !hdr ? 4u : 0u) : 0u);
-    // The descriptors may come from v_readfirstlane (VALU -> SGPR) and the
-    // buffer loads read them inside asm, where hipcc inserts no wait states:
-    // 5 are required (cdna_hip_programming.md 5.7 item 2).
+    // A VALU write of an SGPR (v_readfirstlane) read by a VMEM instruction
+    // needs 5 wait states, and hipcc inserts none before inline asm
+    // (cdna_hip_programming.md 5.7 item 2).  The descriptors are built from
+    // uniform record fields on the scalar unit only, so no s_nop 4 is spent
+    // here (it cost 1-5 %); tools/check_asm_hazards.py, run by build(), fails
+    // the build if a compile ever feeds them from the vector unit.
+#if PRISMDB_SPAN_SNOP
     asm volatile("s_nop 4" : "+s"(rb), "+s"(re));
+#else
+    asm volatile("" : "+s"(rb), "+s"(re));
+#endif
     const int32_t i0 = (int32_t)(t.c * kChunkWords + lane) - (int32_t)pad;
     if (t.c == 0 && pad != 0) {
       // chunk 0: offsets may be negative; give every round its own voffset so
@@ -525,31 +538,42 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
   // Per-stream chain state.
   uint32_t acc[2] = {0u, 0u}, r[2] = {0u, 0u};
 
-  // Start of a chunk: head bytes and the initial-register injection (chunk 0).
-  auto begin = [&](int s, const Task& t, uint32_t (&w)[kRounds], uint32_t e) {
-    if (t.c == 0) {
-      const uint32_t h = t.h();
-      const uint32_t d = h ? readlane(e, 0) | (readlane(e, 1) << 8) | (readlane(e, 2) << 16) : 0u;
-      const uint32_t rr = feed_short(ss, lane, t.r.w ^ kConditioning, d, h);
-      r[s] = rr;
-      acc[s] = 0u;
-      if (t.r.z) {
-        const uint32_t pad = t.pad();
-        const uint32_t inj = lane == (pad & 63u) ? rr : 0u;  // enters with body word 0
-        switch (pad >> 6) {
+  // Start of a chunk: head bytes and the initial register (chunk 0).  The
+  // register enters with body word 0: lane pad%64 of round J = pad/64.
+  //   general kernel: w[J] ^= inj through a 16-way switch on the uniform J
+  //     (an indexed w[J] made hipcc move the ring to scratch); returns 0, J = 0.
+  //   kSkip (log records): returns inj and J, and the fold, which already
+  //     tests every round, applies it under a per-round scalar mask -- the
+  //     switch's compare-and-branch chain cost the WAL rows 6-11 %, while in
+  //     the general kernel a second, masked fold body cost config 3 1.6 %.
+  auto begin = [&](int s, const Task& t, uint32_t (&w)[kRounds], uint32_t e, uint32_t& J) -> uint32_t {
+    J = 0;
+    if (t.c != 0) return 0u;
+    const uint32_t h = t.h();
+    const uint32_t d = h ? readlane(e, 0) | (readlane(e, 1) << 8) | (readlane(e, 2) << 16) : 0u;
+    const uint32_t rr = feed_short(ss, lane, t.r.w ^ kConditioning, d, h);
+    r[s] = rr;
+    acc[s] = 0u;
+    if (t.r.z == 0) return 0u;
+    const uint32_t pad = t.pad();
+    const uint32_t inj = lane == (pad & 63u) ? rr : 0u;
+    if (kSkip) {
+      J = PRISMDB_SPAN_NOSWITCH ? 0u : pad >> 6;
+      return inj;
+    }
+    switch (PRISMDB_SPAN_NOSWITCH ? 0u : pad >> 6) {
 #define PRISMDB_INJ(J) \
   case J:              \
     w[J] ^= inj;       \
     break;
-          PRISMDB_INJ(0) PRISMDB_INJ(1) PRISMDB_INJ(2) PRISMDB_INJ(3) PRISMDB_INJ(4) PRISMDB_INJ(5)
-          PRISMDB_INJ(6) PRISMDB_INJ(7) PRISMDB_INJ(8) PRISMDB_INJ(9) PRISMDB_INJ(10) PRISMDB_INJ(11)
-          PRISMDB_INJ(12) PRISMDB_INJ(13) PRISMDB_INJ(14) PRISMDB_INJ(15)
+      PRISMDB_INJ(0) PRISMDB_INJ(1) PRISMDB_INJ(2) PRISMDB_INJ(3) PRISMDB_INJ(4) PRISMDB_INJ(5)
+      PRISMDB_INJ(6) PRISMDB_INJ(7) PRISMDB_INJ(8) PRISMDB_INJ(9) PRISMDB_INJ(10) PRISMDB_INJ(11)
+      PRISMDB_INJ(12) PRISMDB_INJ(13) PRISMDB_INJ(14) PRISMDB_INJ(15)
 #undef PRISMDB_INJ
-          default:
-            break;
-        }
-      }
+      default:
+        break;
     }
+    return 0u;
   };
   // Slice results: store lanes [0, t.slot()] of stream s's slice ending with task t.
   uint32_t res[2] = {0u, 0u}, bad[2] = {0u, 0u};
@@ -579,8 +603,9 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
   // Fold the pair (stream 0 task tx in wx, stream 1 task ty in wy).
   auto fold = [&](const Task& tx, uint32_t (&wx)[kRounds], uint32_t ex, const Task& ty,
                   uint32_t (&wy)[kRounds], uint32_t ey) {
-    if (!tx.skip()) begin(0, tx, wx, ex);
-    if (!ty.skip()) begin(1, ty, wy, ey);
+    uint32_t Jx = 0, Jy = 0, ix = 0, iy = 0;
+    if (!tx.skip()) ix = begin(0, tx, wx, ex, Jx);
+    if (!ty.skip()) iy = begin(1, ty, wy, ey, Jy);
     uint32_t ax = acc[0], ay = acc[1];
     // kSkip: chunk 0's rounds before round pad/64 hold only padding: acc is 0
     // there and every word is 0, so shift_256(0) ^ 0 leaves acc at 0 and the
@@ -594,18 +619,26 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
     };
     const uint32_t fx = first_round(tx), fy = first_round(ty);
     const uint32_t j0 = kSkip ? (fx < fy ? fx : fy) : 0u;
-    if (j0 == 0) {  // both chunks full (or a multi-chunk span's later chunk): no per-round test
+    if (!kSkip || (j0 == 0 && (Jx | Jy) == 0)) {
+      // General kernel (registers injected by begin), or both registers enter
+      // in round 0 (full chunks, later chunks): straight fold.
+      wx[0] ^= ix;
+      wy[0] ^= iy;
 #pragma unroll
       for (int j = PRISMDB_SPAN_J0; j < kRounds; ++j) {
         ax = step256(lds, tab, ax, wx[j]);
         ay = step256(lds, tab, ay, wy[j]);
       }
     } else {
+      // A padded chunk 0: round j's word takes the injection under a scalar
+      // mask (one v_bitop3 w ^ (inj & m) per round, no branches); with kSkip
+      // the rounds before j0 are skipped.
 #pragma unroll
-      for (int j = PRISMDB_SPAN_J0 > 1 ? PRISMDB_SPAN_J0 : 1; j < kRounds; ++j) {
+      for (int j = 0; j < kRounds; ++j) {
         if ((uint32_t)j >= j0) {
-          ax = step256(lds, tab, ax, wx[j]);
-          ay = step256(lds, tab, ay, wy[j]);
+          const uint32_t mx = (uint32_t)j == Jx ? ~0u : 0u, my = (uint32_t)j == Jy ? ~0u : 0u;
+          ax = step256(lds, tab, ax, __builtin_amdgcn_bitop3_b32(wx[j], ix, mx, 0x78));
+          ay = step256(lds, tab, ay, __builtin_amdgcn_bitop3_b32(wy[j], iy, my, 0x78));
         }
       }
     }

@@ -25,11 +25,14 @@ def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("-D", action="append", default=[])
     ap.add_argument("--keep", help="write the .s here")
+    ap.add_argument("--asm", help="audit this .s (e.g. the build's own) instead of compiling")
+    ap.add_argument("-q", "--quiet", action="store_true", help="print failing kernels only")
     args = ap.parse_args()
-    out = args.keep or tempfile.mktemp(suffix=".s")
-    cmd = ["/opt/rocm/bin/hipcc", "-x", "hip", "--offload-arch=gfx950", "-O3", "-std=c++17",
-           "--cuda-device-only", "-S", SRC, "-o", out] + [f"-D{d}" for d in args.D]
-    subprocess.check_call(cmd)
+    out = args.asm or args.keep or tempfile.mktemp(suffix=".s")
+    if not args.asm:
+        cmd = ["/opt/rocm/bin/hipcc", "-x", "hip", "--offload-arch=gfx950", "-O3", "-std=c++17",
+               "--cuda-device-only", "-S", SRC, "-o", out] + [f"-D{d}" for d in args.D]
+        subprocess.check_call(cmd)
     text = open(out).read().splitlines()
     # kernel bodies: from "<name>:" (a .globl symbol) to ".Lfunc_end"
     kernels, cur, name = {}, None, None
@@ -68,11 +71,12 @@ def main() -> int:
         ok = r1.returncode == 0 and r2.returncode == 0 and spill == 0
         bad += not ok
         short = re.sub(r"^_ZN7prismdb3dev", "", k)[:60]
-        print(f"{'ok ' if ok else 'BAD'} {short:60s} vgpr={info['vgpr_count']} sgpr={info['sgpr_count']} "
-              f"spill={spill} sgpr_spill={info['sgpr_spill_count']} lds={info['group_segment_fixed_size']}")
+        if not (ok and args.quiet):
+            print(f"{'ok ' if ok else 'BAD'} {short:60s} vgpr={info['vgpr_count']} sgpr={info['sgpr_count']} "
+                  f"spill={spill} sgpr_spill={info['sgpr_spill_count']} lds={info['group_segment_fixed_size']}")
         if r1.returncode or r2.returncode:
             print((r1.stdout + r1.stderr + r2.stdout + r2.stderr).strip()[:2000])
-    if not args.keep:
+    if not args.keep and not args.asm:
         os.unlink(out)
     return 1 if bad else 0
 

@@ -86,3 +86,5 @@ for i, l in enumerate(lines):
         if touch <= 20:
             print(f"line {i+1}: {t}   touches pending {sorted(hit)}")
 print(f"{touch} reads of in-flight asm-load registers (linear scan, may include other-branch false positives)")
+
+sys.exit(1 if bad else 0)
