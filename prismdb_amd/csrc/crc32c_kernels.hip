@@ -326,9 +326,21 @@ __device__ __forceinline__ void wait_task(uint32_t (&w)[kRounds], uint32_t& e) {
 //   x = body address bits 0-31          body = first 4-B aligned byte of the span
 //   y = body bits 32-47 | pad << 16 | h << 26 | t << 28 | long << 30
 //   z = body bytes (4W)                 W body words, h head bytes, t tail bytes
-//   w = init
+//   w = register after the head bytes: feed(init ^ ~0, head), computed here
+//       bit-serially by the planner thread (the span kernel used to spend
+//       3 readlanes and a cross-lane GF(2) product per span on it)
 // pad = nch*1024 - W leading zero words of chunk 0 (nch = ceil(W/1024) >= 1).
 // ---------------------------------------------------------------------------
+// Reflected CRC register fed n bytes, one bit at a time (n <= 3 here).
+__device__ __forceinline__ uint32_t feed_bytes(uint32_t r, const uint8_t* p, uint32_t n) {
+  for (uint32_t i = 0; i < n; ++i) {
+    r ^= p[i];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) r = (r >> 1) ^ (kPolyReflected & (0u - (r & 1u)));
+  }
+  return r;
+}
+
 __device__ __forceinline__ SpanRec make_rec(const uint8_t* p, uint32_t len, uint32_t init, bool lng) {
   uint32_t h = (4u - ((uint32_t)(uintptr_t)p & 3u)) & 3u;
   if (h > len) h = len;
@@ -340,7 +352,7 @@ __device__ __forceinline__ SpanRec make_rec(const uint8_t* p, uint32_t len, uint
   r.x = (uint32_t)body;
   r.y = ((uint32_t)(body >> 32) & 0xffffu) | (pad << 16) | (h << 26) | (t << 28) | ((uint32_t)lng << 30);
   r.z = 4u * W;
-  r.w = init;
+  r.w = feed_bytes(init ^ kConditioning, p, h);
   return r;
 }
 
@@ -527,9 +539,9 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
       buf_round<8>(w, rb, v);  buf_round<9>(w, rb, v);  buf_round<10>(w, rb, v); buf_round<11>(w, rb, v);
       buf_round<12>(w, rb, v); buf_round<13>(w, rb, v); buf_round<14>(w, rb, v); buf_round<15>(w, rb, v);
     }
-    const bool first = t.c == 0, last = t.c + 1 == nch;
+    // Edge bytes of the last chunk: tail bytes (lanes 3-5), stored crc (6-9).
+    const bool last = t.c + 1 == nch;
     uint32_t eoff = 0xFFFFFFFFu;
-    if (first && lane < h) eoff = hb + lane;
     if (last && lane >= 3u && lane < 3u + tl) eoff = hb + h + t.r.z + (lane - 3u);
     if (kVerify && last && lane >= 6u && lane < 10u) eoff = (hdr ? 0u : len) + (lane - 6u);
     e = buf_ubyte(re, eoff);
@@ -549,9 +561,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
   auto begin = [&](int s, const Task& t, uint32_t (&w)[kRounds], uint32_t e, uint32_t& J) -> uint32_t {
     J = 0;
     if (t.c != 0) return 0u;
-    const uint32_t h = t.h();
-    const uint32_t d = h ? readlane(e, 0) | (readlane(e, 1) << 8) | (readlane(e, 2) << 16) : 0u;
-    const uint32_t rr = feed_short(ss, lane, t.r.w ^ kConditioning, d, h);
+    const uint32_t rr = t.r.w;  // register after the head bytes (planner)
     r[s] = rr;
     acc[s] = 0u;
     if (t.r.z == 0) return 0u;
