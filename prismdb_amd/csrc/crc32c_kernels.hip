@@ -527,17 +527,28 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
     asm volatile("" : "+s"(rb), "+s"(re));
 #endif
     const int32_t i0 = (int32_t)(t.c * kChunkWords + lane) - (int32_t)pad;
-    if (t.c == 0 && pad != 0) {
-      // chunk 0: offsets may be negative; give every round its own voffset so
-      // the range check sees the wrapped (huge) value, never a wrapped sum
-#pragma unroll
-      for (int j = 0; j < kRounds; ++j) w[j] = buf_dword<0>(rb, (uint32_t)(i0 + 64 * j) * 4u);
-    } else {
+    if (t.c != 0 || pad == 0) {
       const uint32_t v = (uint32_t)i0 * 4u;
       buf_round<0>(w, rb, v);  buf_round<1>(w, rb, v);  buf_round<2>(w, rb, v);  buf_round<3>(w, rb, v);
       buf_round<4>(w, rb, v);  buf_round<5>(w, rb, v);  buf_round<6>(w, rb, v);  buf_round<7>(w, rb, v);
       buf_round<8>(w, rb, v);  buf_round<9>(w, rb, v);  buf_round<10>(w, rb, v); buf_round<11>(w, rb, v);
       buf_round<12>(w, rb, v); buf_round<13>(w, rb, v); buf_round<14>(w, rb, v); buf_round<15>(w, rb, v);
+    } else if (pad <= 64u) {
+      // pad <= 64 (e.g. a 3988-B SST data block): only round 0 can be
+      // negative; rounds 1-15 share one non-negative base with immediate
+      // offsets, 2 address VALUs instead of 16
+      w[0] = buf_dword<0>(rb, (uint32_t)i0 * 4u);
+      const uint32_t v1 = (uint32_t)(i0 + 64) * 4u;
+      w[1] = buf_dword<0>(rb, v1);     w[2] = buf_dword<256>(rb, v1);   w[3] = buf_dword<512>(rb, v1);
+      w[4] = buf_dword<768>(rb, v1);   w[5] = buf_dword<1024>(rb, v1);  w[6] = buf_dword<1280>(rb, v1);
+      w[7] = buf_dword<1536>(rb, v1);  w[8] = buf_dword<1792>(rb, v1);  w[9] = buf_dword<2048>(rb, v1);
+      w[10] = buf_dword<2304>(rb, v1); w[11] = buf_dword<2560>(rb, v1); w[12] = buf_dword<2816>(rb, v1);
+      w[13] = buf_dword<3072>(rb, v1); w[14] = buf_dword<3328>(rb, v1); w[15] = buf_dword<3584>(rb, v1);
+    } else {
+      // chunk 0: offsets may be negative; give every round its own voffset so
+      // the range check sees the wrapped (huge) value, never a wrapped sum
+#pragma unroll
+      for (int j = 0; j < kRounds; ++j) w[j] = buf_dword<0>(rb, (uint32_t)(i0 + 64 * j) * 4u);
     }
     // Edge bytes of the last chunk: tail bytes (lanes 3-5), stored crc (6-9).
     const bool last = t.c + 1 == nch;

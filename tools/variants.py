@@ -101,6 +101,11 @@ def do_run(args, names):
     crc32c.batch(buf, woff, wlen, mask=True, trailer=True, log_header=True)  # log::Writer's header crcs
     wout = torch.empty(nw, dtype=torch.int32, device=dev)
     wmm = torch.empty(nw, dtype=torch.uint8, device=dev)
+    # SST data blocks through descriptors: 3988-B spans (contents + type) at stride 3992
+    ns = (args.gib << 30) // 3992 - 1
+    soff = torch.arange(ns, dtype=torch.int64, device=dev) * 3992
+    slen = torch.full((ns,), 3988, dtype=torch.int32, device=dev)
+    sout = torch.empty(ns, dtype=torch.int32, device=dev)
     al = rng.integers(0, 70000, size=(args.gib << 30) // 35000 // 2).astype(np.int64)
     ao = np.sort(rng.integers(0, (args.gib << 30) // 2 - 70001, size=len(al))).astype(np.int64)
     aoff, alen = torch.from_numpy(ao).to(dev), torch.from_numpy(al.astype(np.int32)).to(dev)
@@ -116,6 +121,8 @@ def do_run(args, names):
         "wal": (lambda n: libs[n][1](buf.data_ptr(), woff.data_ptr(), wlen.data_ptr(), None, nw,
                                      wout.data_ptr(), wmm.data_ptr(), 0x4, sp),
                 int(hlen.sum() + len(hlen)) * nf + nw * (4 + 1 + 12)),
+        "sst3988": (lambda n: libs[n][1](buf.data_ptr(), soff.data_ptr(), slen.data_ptr(), None, ns,
+                                         sout.data_ptr(), None, 0, sp), ns * (3988 + 4 + 12)),
         "adversarial": (lambda n: libs[n][1](buf.data_ptr(), aoff.data_ptr(), alen.data_ptr(), None, len(al),
                                              out.data_ptr(), None, 0, sp), int(al.sum()) + 16 * len(al)),
     }
@@ -131,7 +138,7 @@ def do_run(args, names):
 
     res = {w: {n: [] for n in names} for w in work}
     agree = {}
-    outs_of = {"wal": wout}
+    outs_of = {"wal": wout, "sst3988": sout}
     for w, (fn, _) in work.items():
         ref = None
         for n in names:
