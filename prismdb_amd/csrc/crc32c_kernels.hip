@@ -561,38 +561,37 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
   // Per-stream chain state.
   uint32_t acc[2] = {0u, 0u}, r[2] = {0u, 0u};
 
-  // Start of a chunk: head bytes and the initial register (chunk 0).  The
-  // register enters with body word 0: lane pad%64 of round J = pad/64.
-  //   general kernel: w[J] ^= inj through a 16-way switch on the uniform J
-  //     (an indexed w[J] made hipcc move the ring to scratch); returns 0, J = 0.
-  //   kSkip (log records): returns inj and J, and the fold, which already
-  //     tests every round, applies it under a per-round scalar mask -- the
-  //     switch's compare-and-branch chain cost the WAL rows 6-11 %, while in
-  //     the general kernel a second, masked fold body cost config 3 1.6 %.
-  auto begin = [&](int s, const Task& t, uint32_t (&w)[kRounds], uint32_t e, uint32_t& J) -> uint32_t {
-    J = 0;
+  // Start of a chunk: the initial register (chunk 0), already fed the head
+  // bytes by the planner.  It enters with body word 0: lane pad%64 of round
+  // J = pad/64, a wave-uniform index.  J = 0 (full chunks, pads < 64) is one
+  // XOR; otherwise a rarely taken block puts it into round J's word under a
+  // scalar mask (v_bitop3 w ^ (inj & m)), no branches per round.  (A 16-way
+  // switch on J compiled to a compare tree with register copies at its merges
+  // that every task walked; an indexed w[J] made hipcc move the ring to
+  // scratch.)  kSkip (log records) returns inj and J instead: its fold tests
+  // every round anyway and masks only the 4-5 rounds it folds.
+  auto begin = [&](int s, const Task& t, uint32_t (&w)[kRounds], uint32_t& Jout) -> uint32_t {
+    Jout = 0;
     if (t.c != 0) return 0u;
-    const uint32_t rr = t.r.w;  // register after the head bytes (planner)
+    const uint32_t rr = t.r.w;
     r[s] = rr;
     acc[s] = 0u;
     if (t.r.z == 0) return 0u;
     const uint32_t pad = t.pad();
     const uint32_t inj = lane == (pad & 63u) ? rr : 0u;
+    const uint32_t J = PRISMDB_SPAN_NOSWITCH ? 0u : pad >> 6;
     if (kSkip) {
-      J = PRISMDB_SPAN_NOSWITCH ? 0u : pad >> 6;
+      Jout = J;
       return inj;
     }
-    switch (PRISMDB_SPAN_NOSWITCH ? 0u : pad >> 6) {
-#define PRISMDB_INJ(J) \
-  case J:              \
-    w[J] ^= inj;       \
-    break;
-      PRISMDB_INJ(0) PRISMDB_INJ(1) PRISMDB_INJ(2) PRISMDB_INJ(3) PRISMDB_INJ(4) PRISMDB_INJ(5)
-      PRISMDB_INJ(6) PRISMDB_INJ(7) PRISMDB_INJ(8) PRISMDB_INJ(9) PRISMDB_INJ(10) PRISMDB_INJ(11)
-      PRISMDB_INJ(12) PRISMDB_INJ(13) PRISMDB_INJ(14) PRISMDB_INJ(15)
-#undef PRISMDB_INJ
-      default:
-        break;
+    if (J == 0) {
+      w[0] ^= inj;
+    } else {
+#pragma unroll
+      for (int j = 1; j < kRounds; ++j) {
+        const uint32_t m = (uint32_t)j == J ? ~0u : 0u;
+        w[j] = __builtin_amdgcn_bitop3_b32(w[j], inj, m, 0x78);
+      }
     }
     return 0u;
   };
@@ -624,9 +623,9 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
   // Fold the pair (stream 0 task tx in wx, stream 1 task ty in wy).
   auto fold = [&](const Task& tx, uint32_t (&wx)[kRounds], uint32_t ex, const Task& ty,
                   uint32_t (&wy)[kRounds], uint32_t ey) {
-    uint32_t Jx = 0, Jy = 0, ix = 0, iy = 0;
-    if (!tx.skip()) ix = begin(0, tx, wx, ex, Jx);
-    if (!ty.skip()) iy = begin(1, ty, wy, ey, Jy);
+    uint32_t Jx = 0, Jy = 0, ix = 0, iy = 0;  // kSkip: injections applied in the fold
+    if (!tx.skip()) ix = begin(0, tx, wx, Jx);
+    if (!ty.skip()) iy = begin(1, ty, wy, Jy);
     uint32_t ax = acc[0], ay = acc[1];
     // kSkip: chunk 0's rounds before round pad/64 hold only padding: acc is 0
     // there and every word is 0, so shift_256(0) ^ 0 leaves acc at 0 and the
@@ -641,9 +640,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
     const uint32_t fx = first_round(tx), fy = first_round(ty);
     const uint32_t j0 = kSkip ? (fx < fy ? fx : fy) : 0u;
     if (!kSkip || (j0 == 0 && (Jx | Jy) == 0)) {
-      // General kernel (registers injected by begin), or both registers enter
-      // in round 0 (full chunks, later chunks): straight fold.
-      wx[0] ^= ix;
+      wx[0] ^= ix;  // kSkip, both registers in round 0 (0 otherwise)
       wy[0] ^= iy;
 #pragma unroll
       for (int j = PRISMDB_SPAN_J0; j < kRounds; ++j) {
@@ -651,9 +648,8 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
         ay = step256(lds, tab, ay, wy[j]);
       }
     } else {
-      // A padded chunk 0: round j's word takes the injection under a scalar
-      // mask (one v_bitop3 w ^ (inj & m) per round, no branches); with kSkip
-      // the rounds before j0 are skipped.
+      // kSkip with a padded chunk 0: rounds before j0 skipped, round j's word
+      // takes the injection under a scalar mask (one v_bitop3 w ^ (inj & m))
 #pragma unroll
       for (int j = 0; j < kRounds; ++j) {
         if ((uint32_t)j >= j0) {
