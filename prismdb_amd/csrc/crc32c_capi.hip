@@ -292,6 +292,8 @@ int RunBatch(DeviceCtx& ctx, const SpanBatch& base_args, bool desc, bool verify,
   hipError_t e = hipMemsetAsync(ws.counters, 0, sizeof(SplitCounters), s);
   if (e != hipSuccess) return FailHip(e, "hipMemsetAsync");
   a.skip_above = prismdb::dev::kLongSpan;
+  // span records for the kernel launch_span picks (its chunk size)
+  a.chunk_lg = (a.flags & prismdb::dev::kFlagLogHeader) ? prismdb::dev::kLgChunkWordsLog : 10u;
   a.overflow = &ws.counters->overflow;
   a.rec = ws.rec;
   e = prismdb::dev::launch_plan(a, desc, ws, s);

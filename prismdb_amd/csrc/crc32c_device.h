@@ -20,6 +20,11 @@ constexpr int kWavesPerGroup = 16;                 // 1024-thread workgroup, one
 constexpr int kThreads = kWave * kWavesPerGroup;
 constexpr int kRounds = 16;                        // 256-B rounds per chunk
 constexpr uint32_t kChunkWords = kRounds * kWave;  // 1024 words = 4 KiB per chunk
+// Log-record span kernel chunk.  8 rounds (2 KiB) would make a ~1 KB record one
+// task of 9 loads, but hipcc then copies the ring's in-flight registers
+// (tools/check_inflight.py: 792 sites), so it stays at 16.
+constexpr int kRoundsLog = 16;
+constexpr uint32_t kLgChunkWordsLog = kRoundsLog == 8 ? 9u : 10u;
 constexpr uint32_t kStrideBytes = 4u * kWave;      // 256 B between a lane's words
 constexpr int kCopies = 32;                        // LDS table replication (bank = lane % 32)
 constexpr int kTabWords = 4 * 256 * kCopies;       // 128 KiB of LDS: stride tables
@@ -64,6 +69,7 @@ struct SpanBatch {
   // are runs of equal record counts instead (segment role).
   const uint64_t* slice_start;
   const unsigned long long* nslices_dev;
+  uint32_t chunk_lg;  // planner: log2(chunk words) of the kernel that consumes the span records
 };
 
 struct SplitCounters {

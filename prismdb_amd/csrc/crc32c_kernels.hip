@@ -260,14 +260,23 @@ __device__ __forceinline__ uint32_t asm_load_dword_at(const uint8_t* base, uint3
 // after it (the younger ring buffers) stay in flight; output stores issued in
 // between only make the wait stricter, never short.  The buffer registers are
 // in/out operands so no consumer can be scheduled above the wait.
-template <int kYounger>
-__device__ __forceinline__ void wait_ring(uint32_t (&w)[kRounds]) {
-  asm volatile("s_waitcnt vmcnt(%16)"
-               : "+v"(w[0]), "+v"(w[1]), "+v"(w[2]), "+v"(w[3]), "+v"(w[4]), "+v"(w[5]), "+v"(w[6]),
-                 "+v"(w[7]), "+v"(w[8]), "+v"(w[9]), "+v"(w[10]), "+v"(w[11]), "+v"(w[12]),
-                 "+v"(w[13]), "+v"(w[14]), "+v"(w[15])
-               : "n"(kYounger)
-               : "memory");
+template <int kYounger, int N>
+__device__ __forceinline__ void wait_ring(uint32_t (&w)[N]) {
+  static_assert(N == 16 || N == 8, "ring buffers of 16 (4 KiB chunks) or 8 (2 KiB) words");
+  if constexpr (N == 16) {
+    asm volatile("s_waitcnt vmcnt(%16)"
+                 : "+v"(w[0]), "+v"(w[1]), "+v"(w[2]), "+v"(w[3]), "+v"(w[4]), "+v"(w[5]), "+v"(w[6]),
+                   "+v"(w[7]), "+v"(w[8]), "+v"(w[9]), "+v"(w[10]), "+v"(w[11]), "+v"(w[12]),
+                   "+v"(w[13]), "+v"(w[14]), "+v"(w[15])
+                 : "n"(kYounger)
+                 : "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(%8)"
+                 : "+v"(w[0]), "+v"(w[1]), "+v"(w[2]), "+v"(w[3]), "+v"(w[4]), "+v"(w[5]), "+v"(w[6]),
+                   "+v"(w[7])
+                 : "n"(kYounger)
+                 : "memory");
+  }
 }
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -307,14 +316,27 @@ __device__ __forceinline__ uint32_t buf_ubyte(u32x4 rs, uint32_t voff) {
   return r;
 }
 
-template <int J>
-__device__ __forceinline__ void buf_round(uint32_t (&w)[kRounds], u32x4 rs, uint32_t voff) {
-  w[J] = buf_dword<256 * J>(rs, voff);
+// w[j] = round j at voff + 256 j, j = J..N-1 (immediate offsets).
+template <int N, int J = 0>
+__device__ __forceinline__ void load_rounds(uint32_t (&w)[N], u32x4 rs, uint32_t voff) {
+  if constexpr (J < N) {
+    w[J] = buf_dword<256 * J>(rs, voff);
+    load_rounds<N, J + 1>(w, rs, voff);
+  }
 }
 
-// Wait for a buffer (16 body words + edge) with kYounger loads left in flight.
-template <int kYounger>
-__device__ __forceinline__ void wait_task(uint32_t (&w)[kRounds], uint32_t& e) {
+// w[j] = round j at v1 + 256 (j - 1), j = J..N-1 (rounds from 1 on one base).
+template <int N, int J = 1>
+__device__ __forceinline__ void load_rounds_from1(uint32_t (&w)[N], u32x4 rs, uint32_t v1) {
+  if constexpr (J < N) {
+    w[J] = buf_dword<256 * (J - 1)>(rs, v1);
+    load_rounds_from1<N, J + 1>(w, rs, v1);
+  }
+}
+
+// Wait for a buffer (N body words + edge) with kYounger loads left in flight.
+template <int kYounger, int N>
+__device__ __forceinline__ void wait_task(uint32_t (&w)[N], uint32_t& e) {
   wait_ring<kYounger>(w);
   asm volatile("" : "+v"(e));
 }
@@ -329,7 +351,8 @@ __device__ __forceinline__ void wait_task(uint32_t (&w)[kRounds], uint32_t& e) {
 //   w = register after the head bytes: feed(init ^ ~0, head), computed here
 //       bit-serially by the planner thread (the span kernel used to spend
 //       3 readlanes and a cross-lane GF(2) product per span on it)
-// pad = nch*1024 - W leading zero words of chunk 0 (nch = ceil(W/1024) >= 1).
+// pad = nch*C - W leading zero words of chunk 0 (nch = ceil(W/C) >= 1), C =
+// the consuming kernel's chunk in words (1024; 512 for the log-record kernel).
 // ---------------------------------------------------------------------------
 // Reflected CRC register fed n bytes, one bit at a time (n <= 3 here).
 __device__ __forceinline__ uint32_t feed_bytes(uint32_t r, const uint8_t* p, uint32_t n) {
@@ -341,12 +364,15 @@ __device__ __forceinline__ uint32_t feed_bytes(uint32_t r, const uint8_t* p, uin
   return r;
 }
 
-__device__ __forceinline__ SpanRec make_rec(const uint8_t* p, uint32_t len, uint32_t init, bool lng) {
+// lgc: log2 of the consuming kernel's chunk in words (10: 4 KiB, 9: 2 KiB).
+__device__ __forceinline__ SpanRec make_rec(const uint8_t* p, uint32_t len, uint32_t init, bool lng,
+                                            uint32_t lgc) {
   uint32_t h = (4u - ((uint32_t)(uintptr_t)p & 3u)) & 3u;
   if (h > len) h = len;
   const uint32_t W = (len - h) >> 2, t = (len - h) & 3u;
-  const uint32_t nch = W ? (W + kChunkWords - 1u) / kChunkWords : 1u;
-  const uint32_t pad = (nch * kChunkWords - W) & 1023u;  // W == 0: every load is out of range anyway
+  const uint32_t C = 1u << lgc;
+  const uint32_t nch = W ? (W + C - 1u) >> lgc : 1u;
+  const uint32_t pad = ((nch << lgc) - W) & (C - 1u);  // W == 0: every load is out of range anyway
   const uint64_t body = reinterpret_cast<uint64_t>(p + h);
   SpanRec r;
   r.x = (uint32_t)body;
@@ -374,7 +400,7 @@ struct Task {
   __device__ uint32_t h() const { return (r.y >> 26) & 3u; }
   __device__ uint32_t t() const { return (r.y >> 28) & 3u; }
   __device__ bool lng() const { return (r.y >> 30) & 1u; }
-  __device__ uint32_t nch() const { return r.z ? (r.z + 4095u) >> 12 : 1u; }
+  __device__ uint32_t nch(uint32_t lgb) const { return r.z ? (r.z + (1u << lgb) - 1u) >> lgb : 1u; }
   __device__ uint32_t len() const { return h() + r.z + t(); }
   __device__ const uint8_t* start() const { return body() - h(); }
 };
@@ -391,6 +417,11 @@ struct Task {
 // ---------------------------------------------------------------------------
 template <bool kVerify, bool kSkip>
 __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
+  // Chunk geometry: 4 KiB chunks of 16 rounds; kRoundsLog for the log-record
+  // kernel (crc32c_device.h).
+  constexpr int kR = kSkip ? kRoundsLog : kRounds;
+  constexpr uint32_t kLgC = kSkip ? kLgChunkWordsLog : 10u;  // log2(chunk words)
+  constexpr uint32_t kLgB = kLgC + 2u;         // log2(chunk bytes)
   // Record indices are 32-bit: the host cuts generic batches at kMaxGenericSpans.
   uint32_t n = (uint32_t)a.n;
   if (a.n_dev != nullptr) {
@@ -487,7 +518,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
   SpanRec pend[2];  // record of each stream's pending record
   bool refill[2] = {false, false};
   auto next_task = [&](int s, const Task& t) -> Task {
-    if (!t.skip() && t.c + 1 < t.nch()) {  // a skipped (long) span is one task
+    if (!t.skip() && t.c + 1 < t.nch(kLgB)) {  // a skipped (long) span is one task
       Task u = t;
       u.c = t.c + 1;
       return u;
@@ -507,9 +538,9 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
     }
   };
   // 17 loads, always.
-  auto issue = [&](const Task& t, uint32_t (&w)[kRounds], uint32_t& e) {
+  auto issue = [&](const Task& t, uint32_t (&w)[kR], uint32_t& e) {
     const bool live = !t.skip();
-    const uint32_t pad = t.pad(), h = t.h(), tl = t.t(), nch = t.nch(), len = t.len();
+    const uint32_t pad = t.pad(), h = t.h(), tl = t.t(), nch = t.nch(kLgB), len = t.len();
     // Edge window: [start - hb, start + len + 4) when verifying a trailer after
     // the span, [start - 6, start + len) when the stored crc is a log header.
     const uint32_t hb = kVerify && hdr ? kLogCrcBack : 0u;
@@ -526,29 +557,20 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
 #else
     asm volatile("" : "+s"(rb), "+s"(re));
 #endif
-    const int32_t i0 = (int32_t)(t.c * kChunkWords + lane) - (int32_t)pad;
+    const int32_t i0 = (int32_t)((t.c << kLgC) + lane) - (int32_t)pad;
     if (t.c != 0 || pad == 0) {
-      const uint32_t v = (uint32_t)i0 * 4u;
-      buf_round<0>(w, rb, v);  buf_round<1>(w, rb, v);  buf_round<2>(w, rb, v);  buf_round<3>(w, rb, v);
-      buf_round<4>(w, rb, v);  buf_round<5>(w, rb, v);  buf_round<6>(w, rb, v);  buf_round<7>(w, rb, v);
-      buf_round<8>(w, rb, v);  buf_round<9>(w, rb, v);  buf_round<10>(w, rb, v); buf_round<11>(w, rb, v);
-      buf_round<12>(w, rb, v); buf_round<13>(w, rb, v); buf_round<14>(w, rb, v); buf_round<15>(w, rb, v);
+      load_rounds(w, rb, (uint32_t)i0 * 4u);
     } else if (pad <= 64u) {
       // pad <= 64 (e.g. a 3988-B SST data block): only round 0 can be
-      // negative; rounds 1-15 share one non-negative base with immediate
+      // negative; rounds 1.. share one non-negative base with immediate
       // offsets, 2 address VALUs instead of 16
       w[0] = buf_dword<0>(rb, (uint32_t)i0 * 4u);
-      const uint32_t v1 = (uint32_t)(i0 + 64) * 4u;
-      w[1] = buf_dword<0>(rb, v1);     w[2] = buf_dword<256>(rb, v1);   w[3] = buf_dword<512>(rb, v1);
-      w[4] = buf_dword<768>(rb, v1);   w[5] = buf_dword<1024>(rb, v1);  w[6] = buf_dword<1280>(rb, v1);
-      w[7] = buf_dword<1536>(rb, v1);  w[8] = buf_dword<1792>(rb, v1);  w[9] = buf_dword<2048>(rb, v1);
-      w[10] = buf_dword<2304>(rb, v1); w[11] = buf_dword<2560>(rb, v1); w[12] = buf_dword<2816>(rb, v1);
-      w[13] = buf_dword<3072>(rb, v1); w[14] = buf_dword<3328>(rb, v1); w[15] = buf_dword<3584>(rb, v1);
+      load_rounds_from1(w, rb, (uint32_t)(i0 + 64) * 4u);
     } else {
       // chunk 0: offsets may be negative; give every round its own voffset so
       // the range check sees the wrapped (huge) value, never a wrapped sum
 #pragma unroll
-      for (int j = 0; j < kRounds; ++j) w[j] = buf_dword<0>(rb, (uint32_t)(i0 + 64 * j) * 4u);
+      for (int j = 0; j < kR; ++j) w[j] = buf_dword<0>(rb, (uint32_t)(i0 + 64 * j) * 4u);
     }
     // Edge bytes of the last chunk: tail bytes (lanes 3-5), stored crc (6-9).
     const bool last = t.c + 1 == nch;
@@ -570,7 +592,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
   // that every task walked; an indexed w[J] made hipcc move the ring to
   // scratch.)  kSkip (log records) returns inj and J instead: its fold tests
   // every round anyway and masks only the 4-5 rounds it folds.
-  auto begin = [&](int s, const Task& t, uint32_t (&w)[kRounds], uint32_t& Jout) -> uint32_t {
+  auto begin = [&](int s, const Task& t, uint32_t (&w)[kR], uint32_t& Jout) -> uint32_t {
     Jout = 0;
     if (t.c != 0) return 0u;
     const uint32_t rr = t.r.w;
@@ -588,7 +610,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
       w[0] ^= inj;
     } else {
 #pragma unroll
-      for (int j = 1; j < kRounds; ++j) {
+      for (int j = 1; j < kR; ++j) {
         const uint32_t m = (uint32_t)j == J ? ~0u : 0u;
         w[j] = __builtin_amdgcn_bitop3_b32(w[j], inj, m, 0x78);
       }
@@ -621,8 +643,8 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
     if (t.last()) flush(s, t);
   };
   // Fold the pair (stream 0 task tx in wx, stream 1 task ty in wy).
-  auto fold = [&](const Task& tx, uint32_t (&wx)[kRounds], uint32_t ex, const Task& ty,
-                  uint32_t (&wy)[kRounds], uint32_t ey) {
+  auto fold = [&](const Task& tx, uint32_t (&wx)[kR], uint32_t ex, const Task& ty,
+                  uint32_t (&wy)[kR], uint32_t ey) {
     uint32_t Jx = 0, Jy = 0, ix = 0, iy = 0;  // kSkip: injections applied in the fold
     if (!tx.skip()) ix = begin(0, tx, wx, Jx);
     if (!ty.skip()) iy = begin(1, ty, wy, Jy);
@@ -635,23 +657,23 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
     // interleaved.  Only log-record batches get it: elsewhere the extra
     // scalar state cost config 3 2 % and gained nothing.
     auto first_round = [](const Task& t) -> uint32_t {
-      return (t.skip() || t.r.z == 0u) ? (uint32_t)kRounds : (t.c == 0 ? t.pad() >> 6 : 0u);
+      return (t.skip() || t.r.z == 0u) ? (uint32_t)kR : (t.c == 0 ? t.pad() >> 6 : 0u);
     };
     const uint32_t fx = first_round(tx), fy = first_round(ty);
     const uint32_t j0 = kSkip ? (fx < fy ? fx : fy) : 0u;
     if (!kSkip || (j0 == 0 && (Jx | Jy) == 0)) {
-      wx[0] ^= ix;  // kSkip, both registers in round 0 (0 otherwise)
-      wy[0] ^= iy;
+      // kSkip: both registers enter in round 0 (ix = iy = 0 otherwise); the
+      // ring registers themselves are left untouched
 #pragma unroll
-      for (int j = PRISMDB_SPAN_J0; j < kRounds; ++j) {
-        ax = step256(lds, tab, ax, wx[j]);
-        ay = step256(lds, tab, ay, wy[j]);
+      for (int j = PRISMDB_SPAN_J0; j < kR; ++j) {
+        ax = step256(lds, tab, ax, j == 0 ? wx[0] ^ ix : wx[j]);
+        ay = step256(lds, tab, ay, j == 0 ? wy[0] ^ iy : wy[j]);
       }
     } else {
       // kSkip with a padded chunk 0: rounds before j0 skipped, round j's word
       // takes the injection under a scalar mask (one v_bitop3 w ^ (inj & m))
 #pragma unroll
-      for (int j = 0; j < kRounds; ++j) {
+      for (int j = 0; j < kR; ++j) {
         if ((uint32_t)j >= j0) {
           const uint32_t mx = (uint32_t)j == Jx ? ~0u : 0u, my = (uint32_t)j == Jy ? ~0u : 0u;
           ax = step256(lds, tab, ax, __builtin_amdgcn_bitop3_b32(wx[j], ix, mx, 0x78));
@@ -661,7 +683,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
     }
     acc[0] = ax;
     acc[1] = ay;
-    const bool endx = !tx.skip() && tx.c + 1 == tx.nch(), endy = !ty.skip() && ty.c + 1 == ty.nch();
+    const bool endx = !tx.skip() && tx.c + 1 == tx.nch(kLgB), endy = !ty.skip() && ty.c + 1 == ty.nch(kLgB);
     if (endx && endy) {
       const uint32_t vx = realign(lds, nibtab, ax), vy = realign(lds, nibtab, ay);
       const uint32_t bx = wave_xor(vx), by = wave_xor(vy);
@@ -683,7 +705,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
   // while its loads are in flight.  Fold slot `sl` while the other slot's two
   // tasks are in flight, then refill slot `sl`.
   Task tk[2][2];
-  uint32_t wb[2][2][kRounds];
+  uint32_t wb[2][2][kR];
   uint32_t eb[2][2];
 #pragma unroll
   for (int st = 0; st < 2; ++st) {
@@ -701,7 +723,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
     issue(tk[sl][0], wb[sl][0], eb[sl][0]);
     issue(tk[sl][1], wb[sl][1], eb[sl][1]);
   }
-  constexpr int kYounger = 2 * (kRounds + 1);  // the other slot's two tasks
+  constexpr int kYounger = 2 * (kR + 1);  // the other slot's two tasks
   for (;;) {
 #pragma unroll
     for (int sl = 0; sl < 2; ++sl) {
@@ -907,9 +929,10 @@ __global__ __launch_bounds__(kPlanThreads) void crc32c_plan_kernel(SpanBatch a, 
     const uint32_t init = kDesc ? (a.init != nullptr ? a.init[i] : 0u) : a.init_c;
     const uint8_t* p = a.base + off;
     const bool lng = len > a.skip_above;
-    const SpanRec r = make_rec(p, len, init, lng);
+    const SpanRec r = make_rec(p, len, init, lng, a.chunk_lg);
     ws.rec[i] = r;
-    const uint32_t cnt = lng ? 1u : (r.z ? (r.z + 4095u) >> 12 : 1u);  // Task::nch()
+    const uint32_t lgb = a.chunk_lg + 2u;
+    const uint32_t cnt = lng ? 1u : (r.z ? (r.z + (1u << lgb) - 1u) >> lgb : 1u);  // Task::nch()
     ws.cnt[i] = cnt;
     mine += cnt;
     if (!lng) continue;
@@ -924,9 +947,10 @@ __global__ __launch_bounds__(kPlanThreads) void crc32c_plan_kernel(SpanBatch a, 
     ws.long_span[li] = i;
     ws.long_first[li] = pos;
     ws.long_nseg[li] = nseg;
-    ws.seg_rec[pos] = make_rec(p, first, init, false);
+    // segments: the general kernel (4 KiB chunks) folds them
+    ws.seg_rec[pos] = make_rec(p, first, init, false, 10u);
     for (uint32_t s = 1; s < nseg; ++s)
-      ws.seg_rec[pos + s] = make_rec(p + first + (uint64_t)(s - 1u) * kSegment, kSegment, kConditioning, false);
+      ws.seg_rec[pos + s] = make_rec(p + first + (uint64_t)(s - 1u) * kSegment, kSegment, kConditioning, false, 10u);
   }
   atomicAdd(&sum, (unsigned long long)mine);
   __syncthreads();

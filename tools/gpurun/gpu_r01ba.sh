@@ -1,0 +1,18 @@
+#!/bin/bash
+# A/A: the same library twice, to size the harness bias
+set -o pipefail
+mkdir -p gpurun_out
+
+timeout -k 10 500 python tools/variants.py run --only prev prevcopy --gib 64 --reps 15 > gpurun_out/ba_variants.json 2>gpurun_out/ba_variants.err
+rc=$?
+python - <<'PY'
+import json
+try:
+    d = json.load(open("gpurun_out/ba_variants.json"))
+    print({k: v for k, v in d["agree"].items() if not v})
+    for w, r in d["results"].items():
+        print(w, {n: v["GB/s_median"] for n, v in r.items()})
+except Exception as e:
+    print("variants:", e)
+PY
+exit $rc
