@@ -60,9 +60,10 @@ def test_shard_range_covers_exactly():
                 assert s0 + c0 == s1
 
 
-@pytest.mark.timeout(120)
-def test_gather_world2_gloo():
-    world = 2
+@pytest.mark.timeout(180)
+@pytest.mark.parametrize("world", [2, 4])
+def test_gather_gloo(world):
+    """world 2 and a 4-rank rehearsal of the path bench.py runs at N = 2..8."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
