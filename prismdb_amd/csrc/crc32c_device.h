@@ -23,7 +23,10 @@ constexpr uint32_t kChunkWords = kRounds * kWave;  // 1024 words = 4 KiB per chu
 // Log-record span kernel chunk.  8 rounds (2 KiB) would make a ~1 KB record one
 // task of 9 loads, but hipcc then copies the ring's in-flight registers
 // (tools/check_inflight.py: 792 sites), so it stays at 16.
-constexpr int kRoundsLog = 16;
+#ifndef PRISMDB_ROUNDS_LOG
+#define PRISMDB_ROUNDS_LOG 16
+#endif
+constexpr int kRoundsLog = PRISMDB_ROUNDS_LOG;
 constexpr uint32_t kLgChunkWordsLog = kRoundsLog == 8 ? 9u : 10u;
 constexpr uint32_t kStrideBytes = 4u * kWave;      // 256 B between a lane's words
 constexpr int kCopies = 32;                        // LDS table replication (bank = lane % 32)
