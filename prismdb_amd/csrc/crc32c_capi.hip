@@ -19,8 +19,8 @@
 #ifndef PRISMDB_SPAN_J0
 #define PRISMDB_SPAN_J0 0
 #endif
-#ifndef PRISMDB_SPAN_NOSWITCH
-#define PRISMDB_SPAN_NOSWITCH 0
+#ifndef PRISMDB_SPAN_INJ0
+#define PRISMDB_SPAN_INJ0 0
 #endif
 #include "crc32c_gf2.h"
 
@@ -153,7 +153,7 @@ void InitDevice(DeviceCtx& ctx, int device) {
     ctx.error = t_last_error;
     return;
   }
-#if PRISMDB_SPAN_J0 == 0 && !PRISMDB_SPAN_NOSWITCH  // measurement-only builds compute wrong CRCs on purpose
+#if PRISMDB_SPAN_J0 == 0 && !PRISMDB_SPAN_INJ0  // measurement-only builds compute wrong CRCs on purpose
   ctx.status = SelfTest(ctx);
   if (ctx.status != 0) ctx.error = t_last_error;
 #endif

@@ -18,11 +18,13 @@
 //     lookup address is one v_perm_b32.
 //   * Lane l's stream ends 256-4l bytes before the body end: eight lookups in
 //     lane l's nibble tables apply shift_{256-4l}, then the wave XOR-reduces
-//     with DPP.  The initial register (init, head bytes) enters with body word 0.
+//     with DPP.  The initial register (init fed the head bytes by the planner)
+//     enters with body word 0.
 //   * Persistent grid: one 1024-thread workgroup per CU (the 160 KiB of LDS
-//     tables are loaded once per CU), spans dealt round-robin to waves, two
-//     spans folded per wave at a time (two independent LDS chains), loads
-//     issued with inline asm one pair ahead and retired by counted vmcnt.
+//     tables are loaded once per CU), runs / task-balanced slices of spans
+//     dealt round-robin to the waves' span streams, two spans folded per wave
+//     at a time (two independent LDS chains), loads issued with inline asm
+//     one pair ahead and retired by counted vmcnt.
 //
 // Kernels:
 //   crc32c_fixed_kernel<K, verify>  fixed stride, 4-B aligned, len <= 4 KiB (config 2);
@@ -30,7 +32,9 @@
 //   crc32c_plan_kernel      one thread per span: 16-byte span records (all
 //                           geometry precomputed), long spans cut into segments
 //   crc32c_slice_{scan,mark}_kernel  task-balanced slices of the span records
-//   crc32c_span_kernel      everything else, driven by the span records
+//   crc32c_span_kernel<verify, log>  everything else, driven by the span
+//                           records; the log-record variant skips chunk 0's
+//                           padding rounds
 //   crc32c_combine_kernel   stitches segments back into long spans
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -55,8 +59,8 @@
 #ifndef PRISMDB_SPAN_J0  // measurement knob: span kernel folds rounds >= this only (wrong results)
 #define PRISMDB_SPAN_J0 0
 #endif
-#ifndef PRISMDB_SPAN_NOSWITCH  // measurement knob: initial register always enters round 0 (wrong if pad >= 64)
-#define PRISMDB_SPAN_NOSWITCH 0
+#ifndef PRISMDB_SPAN_INJ0  // measurement knob: initial register always enters round 0 (wrong if pad >= 64)
+#define PRISMDB_SPAN_INJ0 0
 #endif
 #ifndef PRISMDB_SPAN_SNOP  // 1: s_nop 4 between the descriptors and the asm buffer loads
 #define PRISMDB_SPAN_SNOP 0
@@ -601,7 +605,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
     if (t.r.z == 0) return 0u;
     const uint32_t pad = t.pad();
     const uint32_t inj = lane == (pad & 63u) ? rr : 0u;
-    const uint32_t J = PRISMDB_SPAN_NOSWITCH ? 0u : pad >> 6;
+    const uint32_t J = PRISMDB_SPAN_INJ0 ? 0u : pad >> 6;
     if (kSkip) {
       Jout = J;
       return inj;

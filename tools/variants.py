@@ -32,7 +32,7 @@ VARIANTS = {
     "span_j16": {"PRISMDB_SPAN_J0": 16},
     # measurement-only: initial register always in round 0 (wrong where pad >= 64);
     # snop: the s_nop 4 before the span kernel's buffer loads, as it was
-    "noswitch": {"PRISMDB_SPAN_NOSWITCH": 1},
+    "inj0": {"PRISMDB_SPAN_INJ0": 1},
     "snop": {"PRISMDB_SPAN_SNOP": 1},
     # fixed kernel: runs of 16 spans per wave instead of 64
     "run3": {"PRISMDB_RUN_LG": 3},
