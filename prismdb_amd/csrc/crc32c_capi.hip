@@ -67,6 +67,12 @@ void BuildTables(DeviceTables* t) {
   }
   const g::Op s = g::ShiftBytes(prismdb::dev::kSegment);
   for (int i = 0; i < 32; ++i) t->shift_seg[i] = s.col[i];
+  const g::Op s64 = g::ShiftBytes(64ull * prismdb::dev::kSegment);
+  for (int i = 0; i < 32; ++i) t->shift_seg64[i] = s64.col[i];
+  for (int l = 0; l < 64; ++l) {
+    const g::Op m = g::ShiftBytes((63ull - (uint64_t)l) * prismdb::dev::kSegment);
+    for (int i = 0; i < 32; ++i) t->lane_seg[i][l] = m.col[i];
+  }
 }
 
 int RunBatch(DeviceCtx& ctx, const SpanBatch& base_args, bool desc, bool verify, hipStream_t s);

@@ -41,7 +41,9 @@ constexpr uint32_t kSegment = 32u * 1024u;         // ...into pieces of this siz
 struct DeviceTables {
   uint32_t stride[4][256];    // stride[k][b] = shift_256(b << 8k)
   uint32_t lane_nib[8][16][64];  // [n][v][l] = shift_{256-4l}(v << 4n): lane l's realignment
-  uint32_t shift_seg[32];     // column i of shift_kSegment
+  uint32_t shift_seg[32];     // column i of shift_kSegment (M)
+  uint32_t shift_seg64[32];   // column i of M^64
+  uint32_t lane_seg[32][64];  // [i][l] = column i of M^(63-l): lane l's final shift
 };
 
 enum : uint32_t { kRoleSpans = 0, kRoleSegments = 1 };

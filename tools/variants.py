@@ -106,6 +106,11 @@ def do_run(args, names):
     soff = torch.arange(ns, dtype=torch.int64, device=dev) * 3992
     slen = torch.full((ns,), 3988, dtype=torch.int32, device=dev)
     sout = torch.empty(ns, dtype=torch.int32, device=dev)
+    # huge spans: 256 x (64 MiB - 5 B) at odd offsets, 2048 segments each (split path + combine)
+    nh = min(256, (args.gib << 30) // (64 << 20) - 1)
+    hoff_ = torch.arange(nh, dtype=torch.int64, device=dev) * (64 << 20) + 1
+    hlen_ = torch.full((nh,), (64 << 20) - 5, dtype=torch.int32, device=dev)
+    hout = torch.empty(nh, dtype=torch.int32, device=dev)
     al = rng.integers(0, 70000, size=(args.gib << 30) // 35000 // 2).astype(np.int64)
     ao = np.sort(rng.integers(0, (args.gib << 30) // 2 - 70001, size=len(al))).astype(np.int64)
     aoff, alen = torch.from_numpy(ao).to(dev), torch.from_numpy(al.astype(np.int32)).to(dev)
@@ -123,6 +128,8 @@ def do_run(args, names):
                 int(hlen.sum() + len(hlen)) * nf + nw * (4 + 1 + 12)),
         "sst3988": (lambda n: libs[n][1](buf.data_ptr(), soff.data_ptr(), slen.data_ptr(), None, ns,
                                          sout.data_ptr(), None, 0, sp), ns * (3988 + 4 + 12)),
+        "huge64m": (lambda n: libs[n][1](buf.data_ptr(), hoff_.data_ptr(), hlen_.data_ptr(), None, nh,
+                                         hout.data_ptr(), None, 0, sp), nh * ((64 << 20) - 5 + 16)),
         "adversarial": (lambda n: libs[n][1](buf.data_ptr(), aoff.data_ptr(), alen.data_ptr(), None, len(al),
                                              out.data_ptr(), None, 0, sp), int(al.sum()) + 16 * len(al)),
     }
@@ -138,7 +145,7 @@ def do_run(args, names):
 
     res = {w: {n: [] for n in names} for w in work}
     agree = {}
-    outs_of = {"wal": wout, "sst3988": sout}
+    outs_of = {"wal": wout, "sst3988": sout, "huge64m": hout}
     for w, (fn, _) in work.items():
         ref = None
         for n in names:
