@@ -304,10 +304,15 @@ int RunBatch(DeviceCtx& ctx, const SpanBatch& base_args, bool desc, bool verify,
   a.rec = ws.rec;
   e = prismdb::dev::launch_plan(a, desc, ws, s);
   if (e != hipSuccess) return FailHip(e, "plan kernel launch");
-  e = prismdb::dev::launch_slices(a, ws, s);
-  if (e != hipSuccess) return FailHip(e, "slice kernels launch");
-  a.slice_start = ws.slice_start;
-  a.nslices_dev = &ws.counters->nslices;
+  // Task-balanced slices need more records than span streams: with n <= the
+  // stream count every stream holds at most one record either way, and the
+  // two slice kernels' launches are ~9 us of a file-sized call.
+  if (a.n > streams) {
+    e = prismdb::dev::launch_slices(a, ws, s);
+    if (e != hipSuccess) return FailHip(e, "slice kernels launch");
+    a.slice_start = ws.slice_start;
+    a.nslices_dev = &ws.counters->nslices;
+  }
   e = prismdb::dev::launch_span(a, verify, ctx.cus, s);
   if (e != hipSuccess) return FailHip(e, "span kernel launch");
   SpanBatch seg{};
