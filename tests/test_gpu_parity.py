@@ -418,6 +418,55 @@ def test_concurrent_streams(dev, oracle):
         assert (_u32(o) == want).all()
 
 
+def test_concurrent_host_threads(dev, oracle):
+    """Four host threads, each with its own stream, call the generic and the
+    fixed path at once (ctypes drops the GIL): the per-(thread, device, stream)
+    workspaces and the lock-free calls give every thread the oracle's answers."""
+    import threading
+
+    import torch
+    from prismdb_amd import crc32c
+
+    nblk, L = 4096, 4096
+    buf = torch.empty(nblk * L + 64, dtype=torch.uint8, device=dev)
+    crc32c.fill_synthetic(buf, 0x5EED0014)
+    host = buf.cpu().numpy()
+    rng = np.random.default_rng(0x5EED0014)
+    jobs = []
+    for t in range(4):
+        n = 3000 + 500 * t
+        lens = rng.integers(0, 40_000, size=n).astype(np.uint64)
+        off = rng.integers(0, nblk * L - 40_001, size=n).astype(np.uint64)
+        want, _ = oracle.batch(host, off, lens)
+        jobs.append((off, lens, want))
+    want_fixed = oracle.batch_fixed(host, L, L, nblk)
+    errors = []
+
+    def run(t):
+        try:
+            s = torch.cuda.Stream()
+            off, lens, want = jobs[t]
+            with torch.cuda.stream(s):
+                d_off = torch.from_numpy(off.astype(np.int64)).to(dev)
+                d_len = torch.from_numpy(lens.astype(np.uint32).view(np.int32)).to(dev)
+                for _ in range(5):
+                    out, _ = crc32c.batch(buf, d_off, d_len)
+                    outf, _ = crc32c.batch_fixed(buf, L, L, nblk)
+                    s.synchronize()
+                    if not (_u32(out) == want).all() or not (_u32(outf) == want_fixed).all():
+                        errors.append(t)
+                        return
+        except Exception as e:  # noqa: BLE001 - reported below
+            errors.append((t, repr(e)))
+
+    th = [threading.Thread(target=run, args=(t,)) for t in range(4)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join(120)
+    assert not errors, errors
+
+
 def test_host_resident_pipeline(dev, oracle):
     """leveldb_crc32c_batch_host: SST-shaped spans in pageable host memory and
     in a pinned buffer, > 64 MiB so several chunks are in flight; verify mode."""
