@@ -1,0 +1,108 @@
+"""Argument checking of the batch C ABI (include/prismdb_crc32c.h), on CPU.
+
+Every entry point validates its arguments before it touches a device, so
+these run without a GPU: bad arguments give PRISMDB_CRC32C_EINVAL (-1) and a
+thread-local message, an empty batch is a no-op, and -- where no device is
+present -- a valid call fails loudly with PRISMDB_CRC32C_EDEVICE (-2)
+instead of falling back to the CPU.  The reference has no such surface (its
+Extend cannot fail, util/crc32c.h:17); the caller maps a mismatch flag, not
+an error, to Status::Corruption (table/format.cc:99)."""
+import ctypes
+
+import numpy as np
+import pytest
+
+EINVAL, EDEVICE = -1, -2
+MASK, WRITE_TRAILER, LOG_HEADER = 0x1, 0x2, 0x4
+
+
+def _err(native):
+    return native.leveldb_crc32c_last_error().decode()
+
+
+@pytest.fixture()
+def bufs():
+    data = np.zeros(1 << 16, dtype=np.uint8)
+    off = np.arange(4, dtype=np.uint64) * 4096
+    ln = np.full(4, 4000, dtype=np.uint32)
+    out = np.zeros(4, dtype=np.uint32)
+    mm = np.zeros(4, dtype=np.uint8)
+    return data, off, ln, out, mm
+
+
+def test_empty_batches_are_noops(native, bufs):
+    data, off, ln, out, _ = bufs
+    assert native.leveldb_crc32c_batch(None, None, None, None, 0, None, None, 0, None) == 0
+    assert native.leveldb_crc32c_batch_fixed(None, 4096, 4096, 0, 0, None, None, 0, None) == 0
+    assert native.leveldb_crc32c_batch_host(None, None, None, None, 0, None, None, 0) == 0
+
+
+def test_batch_rejects_null_descriptors(native, bufs):
+    data, off, ln, out, _ = bufs
+    rc = native.leveldb_crc32c_batch(data.ctypes.data, None, ln.ctypes.data, None, 4, out.ctypes.data, None, 0,
+                                     None)
+    assert rc == EINVAL and "non-NULL" in _err(native)
+    rc = native.leveldb_crc32c_batch_fixed(None, 4096, 4096, 4, 0, out.ctypes.data, None, 0, None)
+    assert rc == EINVAL and "dev_base" in _err(native)
+
+
+@pytest.mark.parametrize("flags", [0x8, 0x100, 0xFFFFFFF0])
+def test_unknown_flag_bits(native, bufs, flags):
+    data, off, ln, out, _ = bufs
+    rc = native.leveldb_crc32c_batch(data.ctypes.data, off.ctypes.data, ln.ctypes.data, None, 4, out.ctypes.data,
+                                     None, flags, None)
+    assert rc == EINVAL and "flag" in _err(native)
+    rc = native.leveldb_crc32c_batch_fixed(data.ctypes.data, 4096, 4000, 4, 0, out.ctypes.data, None, flags, None)
+    assert rc == EINVAL and "flag" in _err(native)
+
+
+def test_trailer_and_verify_are_exclusive(native, bufs):
+    data, off, ln, out, mm = bufs
+    rc = native.leveldb_crc32c_batch(data.ctypes.data, off.ctypes.data, ln.ctypes.data, None, 4, out.ctypes.data,
+                                     mm.ctypes.data, WRITE_TRAILER, None)
+    assert rc == EINVAL and "exclusive" in _err(native)
+
+
+def test_fixed_length_limit(native, bufs):
+    data, _, _, out, _ = bufs
+    rc = native.leveldb_crc32c_batch_fixed(data.ctypes.data, 1 << 33, 1 << 32, 1, 0, out.ctypes.data, None, 0,
+                                           None)
+    assert rc == EINVAL and "4 GiB" in _err(native)
+
+
+def test_host_batch_checks(native, bufs):
+    data, off, ln, out, mm = bufs
+    p = data.ctypes.data
+    assert native.leveldb_crc32c_batch_host(p, off.ctypes.data, ln.ctypes.data, None, 4, out.ctypes.data, None,
+                                            WRITE_TRAILER) == EINVAL
+    assert "MASK" in _err(native)
+    unsorted = off[::-1].copy()
+    assert native.leveldb_crc32c_batch_host(p, unsorted.ctypes.data, ln.ctypes.data, None, 4, out.ctypes.data,
+                                            None, 0) == EINVAL
+    assert "sorted" in _err(native)
+    big = np.full(4, (64 << 20) + 1, dtype=np.uint32)
+    assert native.leveldb_crc32c_batch_host(p, off.ctypes.data, big.ctypes.data, None, 4, out.ctypes.data, None,
+                                            0) == EINVAL
+    assert "64 MiB" in _err(native)
+    # verify with LOG_HEADER reads 6 bytes before each span: the first may not start before byte 6
+    off0 = np.array([2, 4096], dtype=np.uint64)
+    assert native.leveldb_crc32c_batch_host(p, off0.ctypes.data, ln.ctypes.data, None, 2, out.ctypes.data,
+                                            mm.ctypes.data, LOG_HEADER) == EINVAL
+    assert "header" in _err(native)
+
+
+def test_no_device_fails_loudly(native, bufs):
+    """Without a HIP device a valid call returns EDEVICE and says why; there is
+    no CPU fallback behind the batch entry points."""
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("a HIP device is present")
+    data, off, ln, out, _ = bufs
+    rc = native.leveldb_crc32c_batch(data.ctypes.data, off.ctypes.data, ln.ctypes.data, None, 4, out.ctypes.data,
+                                     None, 0, None)
+    assert rc == EDEVICE, (rc, _err(native))
+    assert _err(native)
+    assert native.leveldb_crc32c_batch_fixed(data.ctypes.data, 4096, 4000, 4, 0, out.ctypes.data, None, 0,
+                                             None) == EDEVICE
+    assert native.leveldb_crc32c_device_init(ctypes.c_int(0)) == EDEVICE
