@@ -65,6 +65,9 @@
 #ifndef PRISMDB_SPAN_SNOP  // 1: s_nop 4 between the descriptors and the asm buffer loads
 #define PRISMDB_SPAN_SNOP 0
 #endif
+#ifndef PRISMDB_LOG_ROUNDSKIP  // log-record kernel: skip chunk 0's padding rounds
+#define PRISMDB_LOG_ROUNDSKIP 1
+#endif
 #ifndef PRISMDB_RUN_LG
 #define PRISMDB_RUN_LG 5  // fixed kernel: log2(pair steps per run); runs of 2 << PRISMDB_RUN_LG spans
 #endif
@@ -425,6 +428,8 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
   // kernel (crc32c_device.h).
   constexpr int kR = kSkip ? kRoundsLog : kRounds;
   constexpr uint32_t kLgC = kSkip ? kLgChunkWordsLog : 10u;  // log2(chunk words)
+  // The log-record kernel skips chunk 0's padding rounds (16-round chunks).
+  constexpr bool kRoundSkip = kSkip && PRISMDB_LOG_ROUNDSKIP;
   constexpr uint32_t kLgB = kLgC + 2u;         // log2(chunk bytes)
   // Record indices are 32-bit: the host cuts generic batches at kMaxGenericSpans.
   uint32_t n = (uint32_t)a.n;
@@ -594,7 +599,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
   // scalar mask (v_bitop3 w ^ (inj & m)), no branches per round.  (A 16-way
   // switch on J compiled to a compare tree with register copies at its merges
   // that every task walked; an indexed w[J] made hipcc move the ring to
-  // scratch.)  kSkip (log records) returns inj and J instead: its fold tests
+  // scratch.)  kRoundSkip (log records) returns inj and J instead: its fold tests
   // every round anyway and masks only the 4-5 rounds it folds.
   auto begin = [&](int s, const Task& t, uint32_t (&w)[kR], uint32_t& Jout) -> uint32_t {
     Jout = 0;
@@ -606,7 +611,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
     const uint32_t pad = t.pad();
     const uint32_t inj = lane == (pad & 63u) ? rr : 0u;
     const uint32_t J = PRISMDB_SPAN_INJ0 ? 0u : pad >> 6;
-    if (kSkip) {
+    if (kRoundSkip) {
       Jout = J;
       return inj;
     }
@@ -649,11 +654,11 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
   // Fold the pair (stream 0 task tx in wx, stream 1 task ty in wy).
   auto fold = [&](const Task& tx, uint32_t (&wx)[kR], uint32_t ex, const Task& ty,
                   uint32_t (&wy)[kR], uint32_t ey) {
-    uint32_t Jx = 0, Jy = 0, ix = 0, iy = 0;  // kSkip: injections applied in the fold
+    uint32_t Jx = 0, Jy = 0, ix = 0, iy = 0;  // kRoundSkip: injections applied in the fold
     if (!tx.skip()) ix = begin(0, tx, wx, Jx);
     if (!ty.skip()) iy = begin(1, ty, wy, Jy);
     uint32_t ax = acc[0], ay = acc[1];
-    // kSkip: chunk 0's rounds before round pad/64 hold only padding: acc is 0
+    // kRoundSkip: chunk 0's rounds before round pad/64 hold only padding: acc is 0
     // there and every word is 0, so shift_256(0) ^ 0 leaves acc at 0 and the
     // rounds are skipped (a ~1 KB log record folds 4-5 rounds, not 16).
     // Skipped tasks and spans without body words fold nothing.  The pair
@@ -664,9 +669,9 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
       return (t.skip() || t.r.z == 0u) ? (uint32_t)kR : (t.c == 0 ? t.pad() >> 6 : 0u);
     };
     const uint32_t fx = first_round(tx), fy = first_round(ty);
-    const uint32_t j0 = kSkip ? (fx < fy ? fx : fy) : 0u;
-    if (!kSkip || (j0 == 0 && (Jx | Jy) == 0)) {
-      // kSkip: both registers enter in round 0 (ix = iy = 0 otherwise); the
+    const uint32_t j0 = kRoundSkip ? (fx < fy ? fx : fy) : 0u;
+    if (!kRoundSkip || (j0 == 0 && (Jx | Jy) == 0)) {
+      // kRoundSkip: both registers enter in round 0 (ix = iy = 0 otherwise); the
       // ring registers themselves are left untouched
 #pragma unroll
       for (int j = PRISMDB_SPAN_J0; j < kR; ++j) {
@@ -674,7 +679,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
         ay = step256(lds, tab, ay, j == 0 ? wy[0] ^ iy : wy[j]);
       }
     } else {
-      // kSkip with a padded chunk 0: rounds before j0 skipped, round j's word
+      // kRoundSkip with a padded chunk 0: rounds before j0 skipped, round j's word
       // takes the injection under a scalar mask (one v_bitop3 w ^ (inj & m))
 #pragma unroll
       for (int j = 0; j < kR; ++j) {
