@@ -11,7 +11,10 @@ import ctypes
 import os
 import threading
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libprismdb_crc32c.so")
+# PRISMDB_LIB: measurement tools (PMC runs of a variant build) may point the
+# package at another build of the same library; unset, the in-tree product.
+LIB_PATH = os.environ.get("PRISMDB_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib",
+                                                           "libprismdb_crc32c.so")
 
 # Every symbol include/prismdb_crc32c.h and include/prismdb_synth.h declare.
 C_ABI_SYMBOLS = (

@@ -33,6 +33,8 @@ VARIANTS = {
     # measurement-only: initial register always in round 0 (wrong where pad >= 64);
     # snop: the s_nop 4 before the span kernel's buffer loads, as it was
     "inj0": {"PRISMDB_SPAN_INJ0": 1},
+    # log-record kernel without the padding-round skip (straight 16-round fold)
+    "noskip": {"PRISMDB_LOG_ROUNDSKIP": 0},
     "snop": {"PRISMDB_SPAN_SNOP": 1},
     # fixed kernel: runs of 16 spans per wave instead of 64
     "run3": {"PRISMDB_RUN_LG": 3},
