@@ -18,6 +18,8 @@ extern "C" {
 
 #define PRISMDB_SST_ECORRUPT (-10)  /* message: the reference's Status text */
 #define PRISMDB_SST_ECAPACITY (-11) /* *n_out holds the count needed */
+#define PRISMDB_SST_EUNSUPPORTED (-12) /* "Not implemented: ...": a snappy-compressed
+                                          index or metaindex block */
 
 /* block kinds */
 #define PRISMDB_SST_DATA 0
@@ -31,9 +33,20 @@ extern "C" {
  * its stored masked CRC in the 4 bytes that follow.  Order: data blocks in
  * index order, filter block (if any), metaindex, index.  The index block's
  * own checksum is verified on the host before it is parsed (a mismatch returns
- * PRISMDB_SST_ECORRUPT, "Corruption: block checksum mismatch").  off/len/kind
- * may be NULL to only count.  Returns 0, PRISMDB_SST_ECORRUPT (reason in
- * leveldb_sst_last_error()) or PRISMDB_SST_ECAPACITY.
+ * PRISMDB_SST_ECORRUPT, "Corruption: block checksum mismatch"), and its type
+ * byte is dispatched as ReadBlock does (table/format.cc:104-146): any type but
+ * kNoCompression/kSnappyCompression is "Corruption: bad block type".
+ *
+ * Limit: the walker does not decompress.  Tables written with
+ * Options::compression = kSnappyCompression (table/table_builder.cc:159) may
+ * hold a snappy index or metaindex block; those return
+ * PRISMDB_SST_EUNSUPPORTED instead of a misparse.  Snappy *data* blocks are
+ * fine: their checksum covers the stored (compressed) bytes.  PrismDB's
+ * default is kNoCompression (include/leveldb/options.h:134).
+ *
+ * off/len/kind may be NULL to only count.  Returns 0, PRISMDB_SST_ECORRUPT,
+ * PRISMDB_SST_EUNSUPPORTED (reason in leveldb_sst_last_error()) or
+ * PRISMDB_SST_ECAPACITY.
  */
 int leveldb_sst_block_spans(const char* file, size_t file_size, uint64_t* off, uint32_t* len,
                             uint8_t* kind, size_t cap, size_t* n_out);

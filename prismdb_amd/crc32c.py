@@ -20,6 +20,7 @@ Status::Corruption("block checksum mismatch"), see prismdb_amd.sst.
 """
 from __future__ import annotations
 
+from contextlib import nullcontext as _nullcontext
 from typing import Optional, Tuple
 
 from ._lib import check, lib
@@ -110,13 +111,26 @@ def batch_fixed(buf, stride: int, length: int, nblocks: int, init: int = 0, *, m
     return out, (mismatch if verify else None)
 
 
+def _span_reach(log_header: bool, verify: bool, trailer: bool) -> Tuple[int, int]:
+    """(bytes read or written before a span, bytes after it): the stored log
+    header (6 B before, LOG_HEADER with verify or trailer) or the 4-byte block
+    trailer after it (verify or trailer without LOG_HEADER)."""
+    touches = verify or trailer
+    return (6 if touches and log_header else 0), (4 if touches and not log_header else 0)
+
+
 def batch(buf, off, lens, init=None, *, mask: bool = False, verify: bool = False, out=None,
-          mismatch=None, stream=None, trailer: bool = False,
-          log_header: bool = False) -> Tuple[object, Optional[object]]:
+          mismatch=None, stream=None, trailer: bool = False, log_header: bool = False,
+          check_bounds: bool = True) -> Tuple[object, Optional[object]]:
     """CRC32C of arbitrary spans buf[off[i] : off[i]+lens[i]] (int64 off, int32 lens, int32 init).
 
     trailer=True also stores each (masked, with mask=True) result as 4 LE bytes
-    right after its span (TableBuilder::WriteRawBlock)."""
+    right after its span (TableBuilder::WriteRawBlock).
+
+    check_bounds: every span, with its stored trailer or log header, must lie
+    inside buf (ValueError otherwise; a bad descriptor would be a device
+    fault).  The check is one device reduction and a host sync; callers that
+    reuse descriptors they have already checked may pass False."""
     if trailer and verify:
         raise ValueError("trailer and verify are exclusive")
     torch = _torch()
@@ -127,6 +141,14 @@ def batch(buf, off, lens, init=None, *, mask: bool = False, verify: bool = False
     if off.dtype != torch.int64 or lens.dtype != torch.int32 or (init is not None and init.dtype != torch.int32):
         raise TypeError("off must be int64, lens/init int32 (uint32 bit patterns)")
     off, lens = off.contiguous(), lens.contiguous()
+    if check_bounds and n:
+        lead, tail = _span_reach(log_header, verify, trailer)
+        with torch.cuda.stream(stream) if stream is not None else _nullcontext():
+            end = off + (lens.to(torch.int64) & 0xFFFFFFFF)
+            lo, hi = torch.stack([off.min(), end.max()]).tolist()
+        if lo < lead or hi + tail > buf.numel() * buf.element_size():
+            raise ValueError(f"spans reach [{lo - lead}, {hi + tail}) outside buf "
+                             f"({buf.numel() * buf.element_size()} bytes)")
     init = init.contiguous() if init is not None else None
     if out is None:
         out = torch.empty(n, dtype=torch.int32, device=buf.device)
@@ -151,6 +173,14 @@ def batch_host(base, off, lens, init=None, *, mask: bool = False, verify: bool =
     off = np.ascontiguousarray(off, dtype=np.uint64)
     lens = np.ascontiguousarray(lens, dtype=np.uint32)
     ini = np.ascontiguousarray(init, dtype=np.uint32) if init is not None else None
+    if len(lens) != n or (ini is not None and len(ini) != n):
+        raise ValueError("off, lens and init must have the same length")
+    nbytes = base.numel() * base.element_size() if hasattr(base, "data_ptr") else base.nbytes
+    if n:
+        lead, tail = _span_reach(log_header, verify, False)
+        lo, hi = int(off.min()), int((off + lens.astype(np.uint64)).max())
+        if lo < lead or hi + tail > nbytes:
+            raise ValueError(f"spans reach [{lo - lead}, {hi + tail}) outside the host buffer ({nbytes} bytes)")
     out = np.empty(n, dtype=np.uint32)
     mm = np.empty(n, dtype=np.uint8) if verify else None
     ptr = base.data_ptr() if hasattr(base, "data_ptr") else base.ctypes.data

@@ -41,6 +41,11 @@ constexpr size_t kSlotBytes = kMaxSpan + 8;  // a chunk holds one span of up to 
 constexpr size_t kChunkSpans = 1u << 16;     // descriptors per chunk
 constexpr int kDepth = 4;
 
+// Test hook (not in the public header, like prismdb_crc32c_force_generic):
+// the k-th chunk of every later call fails as a device error would, after the
+// earlier chunks have been enqueued.  0 = off.
+int g_fail_after_chunks = 0;
+
 int PipeFail(int code, const std::string& msg) {
   prismdb::SetLastError(msg);
   return code;
@@ -200,6 +205,20 @@ int leveldb_crc32c_batch_host(const void* host_base, const uint64_t* off, const 
   const uint8_t* src = static_cast<const uint8_t*>(host_base);
   const bool pinned = IsPinned(host_base);
 
+  // Abandon the call: wait for everything this call enqueued (DMAs may still
+  // read the caller's source, kernels and D2H copies still write the slots)
+  // and release every slot without copying anything out, so that the next
+  // call on this thread's ring starts empty.  Returns the original failure.
+  auto abort_call = [&](int code) -> int {
+    const std::string msg = leveldb_crc32c_last_error();
+    (void)hipStreamSynchronize(ring->copy);
+    (void)hipStreamSynchronize(ring->compute);
+    (void)hipGetLastError();
+    for (Slot& q : ring->slot) q.busy = false;
+    prismdb::SetLastError(msg);
+    return code;
+  };
+
   // Retire a slot: wait until the compute stream released it, hand its
   // results to the caller.
   auto retire = [&](Slot& s) -> int {
@@ -213,10 +232,10 @@ int leveldb_crc32c_batch_host(const void* host_base, const uint64_t* off, const 
   };
 
   size_t i = 0;
-  int k = 0;
+  int k = 0, chunks = 0;
   while (i < n) {
     Slot& s = ring->slot[k];
-    if ((rc = retire(s)) != 0) return rc;
+    if ((rc = retire(s)) != 0) return abort_call(rc);
     // Chunk: consecutive spans whose bytes (plus trailers) fit kChunkBytes;
     // a single span may be larger (up to kMaxSpan).
     const uint64_t lo = off[i] - lead;
@@ -251,14 +270,18 @@ int leveldb_crc32c_batch_host(const void* host_base, const uint64_t* off, const 
     if (e == hipSuccess)
       e = hipMemcpyAsync(s.d_desc, s.h_desc, cnt * (init ? 16 : 12), hipMemcpyHostToDevice, ring->compute);
     if (e == hipSuccess) e = hipStreamWaitEvent(ring->compute, s.copied, 0);
-    if (e != hipSuccess) return PipeFail(PRISMDB_CRC32C_EDEVICE, std::string("pipeline H2D: ") + hipGetErrorString(e));
-    rc = leveldb_crc32c_batch(s.d_data, d_off, d_len, init ? d_init : nullptr, cnt, s.d_out,
-                              mismatch ? s.d_mm : nullptr, flags, ring->compute);
-    if (rc != 0) return rc;  // message already set by leveldb_crc32c_batch
+    if (e != hipSuccess)
+      return abort_call(PipeFail(PRISMDB_CRC32C_EDEVICE, std::string("pipeline H2D: ") + hipGetErrorString(e)));
+    rc = g_fail_after_chunks > 0 && ++chunks >= g_fail_after_chunks
+             ? PipeFail(PRISMDB_CRC32C_EDEVICE, "pipeline: injected failure (prismdb_pipeline_fail_after)")
+             : leveldb_crc32c_batch(s.d_data, d_off, d_len, init ? d_init : nullptr, cnt, s.d_out,
+                                    mismatch ? s.d_mm : nullptr, flags, ring->compute);
+    if (rc != 0) return abort_call(rc);  // message already set by leveldb_crc32c_batch
     e = hipMemcpyAsync(s.h_out, s.d_out, cnt * 4, hipMemcpyDeviceToHost, ring->compute);
     if (e == hipSuccess && mismatch) e = hipMemcpyAsync(s.h_mm, s.d_mm, cnt, hipMemcpyDeviceToHost, ring->compute);
     if (e == hipSuccess) e = hipEventRecord(s.done, ring->compute);
-    if (e != hipSuccess) return PipeFail(PRISMDB_CRC32C_EDEVICE, std::string("pipeline D2H: ") + hipGetErrorString(e));
+    if (e != hipSuccess)
+      return abort_call(PipeFail(PRISMDB_CRC32C_EDEVICE, std::string("pipeline D2H: ") + hipGetErrorString(e)));
     s.busy = true;
     s.first = i;
     s.count = cnt;
@@ -266,8 +289,10 @@ int leveldb_crc32c_batch_host(const void* host_base, const uint64_t* off, const 
     k = (k + 1) % kDepth;
   }
   for (int q = 0; q < kDepth; ++q)
-    if ((rc = retire(ring->slot[(k + q) % kDepth])) != 0) return rc;
+    if ((rc = retire(ring->slot[(k + q) % kDepth])) != 0) return abort_call(rc);
   return 0;
 }
+
+void prismdb_pipeline_fail_after(int chunks) { g_fail_after_chunks = chunks > 0 ? chunks : 0; }
 
 }  // extern "C"

@@ -61,6 +61,23 @@ int Corrupt(const std::string& why) {
   return PRISMDB_SST_ECORRUPT;
 }
 
+// Status::NotSupported's text (util/status.cc: "Not implemented: ").
+int Unsupported(const std::string& what) {
+  t_sst_error = "Not implemented: " + what;
+  return PRISMDB_SST_EUNSUPPORTED;
+}
+
+// Block types, table/format.h (CompressionType, include/leveldb/options.h:25-31).
+constexpr uint8_t kNoCompression = 0;
+constexpr uint8_t kSnappyCompression = 1;
+
+// ReadBlock's verify for one block on the host: contents || type against the
+// stored masked CRC that follows (table/format.cc:93-101).
+bool HostVerify(const uint8_t* block, uint64_t size) {
+  return leveldb::crc32c::Unmask(Le32(block + size + 1)) ==
+         leveldb::crc32c::Value(reinterpret_cast<const char*>(block), (size_t)size + 1);
+}
+
 struct Table {
   const uint8_t* file;
   size_t size;
@@ -116,11 +133,14 @@ int leveldb_sst_block_spans(const char* file, size_t file_size, uint64_t* off, u
   const Table t{f, file_size};
   if (!t.Fits(index) || !t.Fits(meta)) return Corrupt("truncated block read");
 
-  // The index is parsed here, so verify it first (ReadBlock, table/format.cc:93-101).
+  // The index is parsed here, so verify it first (ReadBlock, table/format.cc:93-101),
+  // then dispatch on its type byte as ReadBlock does (:104-146).  Snappy
+  // blocks (Options::compression = kSnappyCompression, table_builder.cc:159)
+  // would need decompression before parsing, which this walker does not do.
   const uint8_t* ib = f + index.offset;
-  if (leveldb::crc32c::Unmask(Le32(ib + index.size + 1)) !=
-      leveldb::crc32c::Value(reinterpret_cast<const char*>(ib), (size_t)index.size + 1))
-    return Corrupt("block checksum mismatch");
+  if (!HostVerify(ib, index.size)) return Corrupt("block checksum mismatch");
+  if (ib[index.size] == kSnappyCompression) return Unsupported("snappy-compressed index block");
+  if (ib[index.size] != kNoCompression) return Corrupt("bad block type");
 
   std::vector<Handle> spans;
   std::vector<uint8_t> kinds;
@@ -136,19 +156,23 @@ int leveldb_sst_block_spans(const char* file, size_t file_size, uint64_t* off, u
 
   // Metaindex: "filter.<name>" -> filter block.  Its own trailer is part of
   // the batch, so a damaged metaindex shows up as a mismatch; it is only
-  // walked if it parses.
+  // walked if it is stored uncompressed and parses.  A snappy metaindex with a
+  // good checksum hides the filter block's handle: unsupported, as above.
   const uint8_t* mb = f + meta.offset;
-  ForEachEntry(mb, (size_t)meta.size, [&](const std::string& key, const uint8_t* v, size_t vn) {
-    if (key.compare(0, 7, "filter.") == 0) {
-      Handle h;
-      const uint8_t* q = v;
-      if (ReadHandle(q, v + vn, &h) && t.Fits(h)) {
-        spans.push_back(h);
-        kinds.push_back(PRISMDB_SST_FILTER);
+  if (mb[meta.size] == kSnappyCompression && HostVerify(mb, meta.size))
+    return Unsupported("snappy-compressed metaindex block");
+  if (mb[meta.size] == kNoCompression)
+    ForEachEntry(mb, (size_t)meta.size, [&](const std::string& key, const uint8_t* v, size_t vn) {
+      if (key.compare(0, 7, "filter.") == 0) {
+        Handle h;
+        const uint8_t* q = v;
+        if (ReadHandle(q, v + vn, &h) && t.Fits(h)) {
+          spans.push_back(h);
+          kinds.push_back(PRISMDB_SST_FILTER);
+        }
       }
-    }
-    return true;
-  });
+      return true;
+    });
   spans.push_back(meta);
   kinds.push_back(PRISMDB_SST_METAINDEX);
   spans.push_back(index);

@@ -175,14 +175,20 @@ def read_log(image, *, checksum: bool = True, initial_offset: int = 0) -> LogRea
     return read_logs([image], checksum=checksum, initial_offsets=[initial_offset])[0]
 
 
-def seal_log(buf, header_off, length, *, stream=None):
+def seal_log(buf, header_off, length, *, stream=None, check_bounds: bool = True):
     """Write log::Writer's header checksum (db/log_writer.cc:90-97) in place.
 
     buf: device uint8 tensor of log blocks whose physical records have their
     length and type bytes filled in; header_off (int64) / length (int32) name
     the records.  Bytes [h, h+4) of each header get Mask(crc32c(type ||
-    payload)).  Returns the masked CRCs (int32)."""
-    span_off = header_off + 6
-    span_len = length + 1
-    out, _ = crc32c.batch(buf, span_off, span_len, mask=True, trailer=True, log_header=True, stream=stream)
+    payload)).  Returns the masked CRCs (int32).  Everything runs on `stream`
+    (default: torch's current stream)."""
+    import torch
+    from contextlib import nullcontext
+
+    with torch.cuda.stream(stream) if stream is not None else nullcontext():
+        span_off = header_off + 6
+        span_len = length + 1
+        out, _ = crc32c.batch(buf, span_off, span_len, mask=True, trailer=True, log_header=True,
+                              check_bounds=check_bounds)
     return out

@@ -14,6 +14,7 @@ device through leveldb_crc32c_batch.
 from __future__ import annotations
 
 import ctypes
+from contextlib import nullcontext
 from dataclasses import dataclass
 from typing import List, Sequence
 
@@ -23,12 +24,26 @@ from ._lib import lib
 KIND_NAMES = {0: "data", 1: "filter", 2: "metaindex", 3: "index"}
 SST_ECORRUPT = -10
 SST_ECAPACITY = -11
+SST_EUNSUPPORTED = -12
 OK = "OK"
 MISMATCH = "Corruption: block checksum mismatch"  # table/format.cc:99
 
 
-class SstCorruption(Exception):
+class SstError(Exception):
+    """A table whose blocks cannot be listed; str() is the reference's Status text."""
+
+
+class SstCorruption(SstError):
     """Status::Corruption raised while walking the table layout."""
+
+
+class SstUnsupported(SstError):
+    """Status::NotSupported: a snappy-compressed index or metaindex block
+    (the walker does not decompress; include/prismdb_sst.h)."""
+
+
+def _raise(rc: int, msg: str):
+    raise (SstUnsupported if rc == SST_EUNSUPPORTED else SstCorruption)(msg)
 
 
 def _sst_lib():
@@ -50,14 +65,14 @@ def block_spans(image: bytes):
     n = ctypes.c_size_t(0)
     rc = L.leveldb_sst_block_spans(image, len(image), None, None, None, 0, ctypes.byref(n))
     if rc not in (0, SST_ECAPACITY):
-        raise SstCorruption(L.leveldb_sst_last_error().decode())
+        _raise(rc, L.leveldb_sst_last_error().decode())
     off = np.empty(n.value, dtype=np.uint64)
     ln = np.empty(n.value, dtype=np.uint32)
     kind = np.empty(n.value, dtype=np.uint8)
     rc = L.leveldb_sst_block_spans(image, len(image), off.ctypes.data, ln.ctypes.data, kind.ctypes.data, n.value,
                                    ctypes.byref(n))
     if rc != 0:
-        raise SstCorruption(L.leveldb_sst_last_error().decode())
+        _raise(rc, L.leveldb_sst_last_error().decode())
     return off, ln, kind
 
 
@@ -73,7 +88,7 @@ class BlockStatus:
 @dataclass
 class VerifyResult:
     blocks: List[BlockStatus]
-    table_errors: List[str]  # per table: "" or the layout Corruption text
+    table_errors: List[str]  # per table: "" or the layout Status text (Corruption / Not implemented)
 
     @property
     def ok(self) -> bool:
@@ -100,7 +115,7 @@ def verify_tables(images: Sequence[bytes], device=None, stream=None) -> VerifyRe
         try:
             o, ln, k = block_spans(img)
             errors.append("")
-        except SstCorruption as e:
+        except SstError as e:
             o, ln, k = (np.empty(0, np.uint64), np.empty(0, np.uint32), np.empty(0, np.uint8))
             errors.append(str(e))
         offs.append(o + np.uint64(base))
@@ -117,11 +132,14 @@ def verify_tables(images: Sequence[bytes], device=None, stream=None) -> VerifyRe
     tab = np.concatenate(tabs) if tabs else np.empty(0, np.int64)
     blocks: List[BlockStatus] = []
     if len(off):
-        d_buf = torch.from_numpy(blob).to(dev, non_blocking=True)
-        d_off = torch.from_numpy(off.astype(np.int64)).to(dev)
-        d_len = torch.from_numpy(ln.view(np.int32)).to(dev)
-        _, mm = crc32c.batch(d_buf, d_off, d_len, verify=True, stream=stream)
-        bad = mm.cpu().numpy()
+        # copies, batch and readback all on one stream (torch's current one
+        # unless the caller names another), so each waits for the one before
+        with torch.cuda.stream(stream) if stream is not None else nullcontext():
+            d_buf = torch.from_numpy(blob).to(dev, non_blocking=True)
+            d_off = torch.from_numpy(off.astype(np.int64)).to(dev)
+            d_len = torch.from_numpy(ln.view(np.int32)).to(dev)
+            _, mm = crc32c.batch(d_buf, d_off, d_len, verify=True)
+            bad = mm.cpu().numpy()
         for i in range(len(off)):
             t = int(tab[i])
             blocks.append(BlockStatus(t, KIND_NAMES[int(kind[i])], int(off[i]) - bases[t], int(ln[i]) - 1,
@@ -135,6 +153,9 @@ def seal_blocks(buf, off, size, *, stream=None):
     buf: device uint8 tensor holding blocks at off[i] (int64) with size[i]
     (int32) content bytes, the type byte already at off[i]+size[i]; the 4
     bytes after it are overwritten.  Returns the masked CRCs (int32)."""
-    lens = (size.to(dtype=size.dtype) + 1)
-    out, _ = crc32c.batch(buf, off, lens, mask=True, stream=stream, trailer=True)
+    import torch
+
+    with torch.cuda.stream(stream) if stream is not None else nullcontext():
+        lens = size + 1
+        out, _ = crc32c.batch(buf, off, lens, mask=True, trailer=True)
     return out

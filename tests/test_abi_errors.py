@@ -106,3 +106,24 @@ def test_no_device_fails_loudly(native, bufs):
     assert native.leveldb_crc32c_batch_fixed(data.ctypes.data, 4096, 4000, 4, 0, out.ctypes.data, None, 0,
                                              None) == EDEVICE
     assert native.leveldb_crc32c_device_init(ctypes.c_int(0)) == EDEVICE
+
+
+def test_python_host_batch_bounds(native):
+    """prismdb_amd.crc32c.batch_host checks descriptors against the host buffer
+    before calling the engine: spans (with their stored trailer or log header)
+    inside the buffer, equal-length descriptor arrays."""
+    from prismdb_amd import crc32c
+
+    data = np.zeros(8192, dtype=np.uint8)
+    off = np.array([0, 4096], dtype=np.uint64)
+    with pytest.raises(ValueError, match="outside"):
+        crc32c.batch_host(data, off, np.array([4096, 4097], dtype=np.uint32))
+    with pytest.raises(ValueError, match="outside"):  # the verify trailer of the last span
+        crc32c.batch_host(data, off, np.array([4000, 4093], dtype=np.uint32), verify=True)
+    with pytest.raises(ValueError, match="outside"):  # the log header before the first span
+        crc32c.batch_host(data, np.array([3, 100], dtype=np.uint64), np.array([10, 10], dtype=np.uint32),
+                          verify=True, log_header=True)
+    with pytest.raises(ValueError, match="same length"):
+        crc32c.batch_host(data, off, np.array([10], dtype=np.uint32))
+    with pytest.raises(ValueError, match="same length"):
+        crc32c.batch_host(data, off, np.array([10, 10], dtype=np.uint32), init=np.array([1], dtype=np.uint32))

@@ -27,7 +27,7 @@ def _u32(t):
 def _to_dev(arr, dev):
     import torch
 
-    return torch.from_numpy(np.ascontiguousarray(arr)).to(dev)
+    return torch.from_numpy(np.array(arr, copy=True)).to(dev)
 
 
 def test_golden_sweep_device(dev, golden):
@@ -519,3 +519,40 @@ def test_host_pipeline_mixed_large_spans(dev, oracle):
     host[int(off[302]) + 12345678] ^= 0x10
     _, mm = crc32c.batch_host(host, off, lens, verify=True)
     assert np.nonzero(mm)[0].tolist() == [302]
+
+
+def test_host_pipeline_failure_drains_ring(dev, oracle):
+    """A host batch that fails after several chunks are in flight leaves the
+    thread's ring empty: the next, smaller call on the same thread gets its own
+    results only and nothing is written past its output arrays."""
+    import ctypes
+
+    from prismdb_amd import _lib, crc32c
+
+    L = _lib.lib()
+    L.prismdb_pipeline_fail_after.argtypes = [ctypes.c_int]
+    n = 40000  # ~152 MiB at stride 3992: five 32 MiB chunks
+    off = np.arange(n, dtype=np.uint64) * 3992
+    lens = np.full(n, 3988, dtype=np.uint32)
+    host = oracle.synth(n * 3992 + 8, 0x5EED0010)
+    L.prismdb_pipeline_fail_after(3)
+    try:
+        with pytest.raises(RuntimeError, match="injected failure"):
+            crc32c.batch_host(host, off, lens, verify=True)
+    finally:
+        L.prismdb_pipeline_fail_after(0)
+    m, guard = 100, 4096
+    out = np.full(m + guard, 0xA5A5A5A5, dtype=np.uint32)
+    mm = np.full(m + guard, 0x5A, dtype=np.uint8)
+    rc = L.leveldb_crc32c_batch_host(ctypes.c_void_p(host.ctypes.data), ctypes.c_void_p(off.ctypes.data),
+                                     ctypes.c_void_p(lens.ctypes.data), None, ctypes.c_size_t(m),
+                                     ctypes.c_void_p(out.ctypes.data), ctypes.c_void_p(mm.ctypes.data),
+                                     ctypes.c_uint32(0))
+    assert rc == 0, L.leveldb_crc32c_last_error()
+    want, _ = oracle.batch(host, off[:m], lens[:m])
+    np.testing.assert_array_equal(out[:m], want)
+    assert (out[m:] == 0xA5A5A5A5).all() and (mm[m:] == 0x5A).all()
+    # and a full call afterwards is whole again
+    got, _ = crc32c.batch_host(host, off, lens)
+    want, _ = oracle.batch(host, off, lens)
+    np.testing.assert_array_equal(got, want)

@@ -99,3 +99,48 @@ def test_seal_long_block_split_path(native, oracle):
     want = oracle.mask(oracle.value(host[:n + 1].tobytes()))
     assert int.from_bytes(out[n + 1:n + 5].tobytes(), "little") == want
     assert (out[:n + 1] == host[:n + 1]).all() and (out[n + 5:] == host[n + 5:]).all()
+
+
+def _retype(f: bytearray, blk: dict, typ: int, oracle) -> None:
+    """Set a block's type byte and reseal its trailer (a well-formed block of that type)."""
+    o, n = blk["offset"], blk["size"]
+    f[o + n] = typ
+    crc = oracle.mask(oracle.value(bytes(f[o:o + n + 1])))
+    f[o + n + 1:o + n + 5] = crc.to_bytes(4, "little")
+
+
+@pytest.mark.parametrize("kind", ["index", "metaindex"])
+def test_block_spans_snappy_index_unsupported(native, golden, oracle, kind):
+    """A table built with kSnappyCompression may store its index/metaindex
+    compressed (table/table_builder.cc:159): reported as NotSupported, never
+    parsed as raw entries."""
+    from prismdb_amd import sst
+
+    f = bytearray(golden["sst_bytes"])
+    blk = [b for b in golden["sst"]["blocks"] if b["kind"] == kind][0]
+    _retype(f, blk, 1, oracle)
+    with pytest.raises(sst.SstUnsupported, match=f"Not implemented: snappy-compressed {kind} block"):
+        sst.block_spans(bytes(f))
+
+
+def test_block_spans_bad_index_type(native, golden, oracle):
+    """ReadBlock's default case (table/format.cc:141-145)."""
+    from prismdb_amd import sst
+
+    f = bytearray(golden["sst_bytes"])
+    blk = [b for b in golden["sst"]["blocks"] if b["kind"] == "index"][0]
+    _retype(f, blk, 7, oracle)
+    with pytest.raises(sst.SstCorruption, match="Corruption: bad block type"):
+        sst.block_spans(bytes(f))
+
+
+def test_block_spans_damaged_metaindex_type_left_to_batch(native, golden):
+    """A damaged metaindex type byte fails its checksum: the walker still lists
+    the table (the batch flags the metaindex), as before."""
+    from prismdb_amd import sst
+
+    f = bytearray(golden["sst_bytes"])
+    meta = [b for b in golden["sst"]["blocks"] if b["kind"] == "metaindex"][0]
+    f[meta["offset"] + meta["size"]] ^= 1  # type 0 -> 1, trailer not resealed
+    off, ln, kind = sst.block_spans(bytes(f))
+    assert [sst.KIND_NAMES[int(k)] for k in kind].count("metaindex") == 1

@@ -43,10 +43,10 @@ def main():
     d_off = torch.from_numpy(off).to(dev)
     d_len = torch.full((nd,), 3988, dtype=torch.int32, device=dev)
     out = torch.empty(nd + 1, dtype=torch.int32, device=dev)
-    res["data_blocks_desc_us"] = timed(lambda: crc32c.batch(buf, d_off, d_len, out=out[:nd]))
+    res["data_blocks_desc_us"] = timed(lambda: crc32c.batch(buf, d_off, d_len, out=out[:nd], check_bounds=False))
     off2 = torch.from_numpy(np.concatenate([off, [nd * 3992]])).to(dev)
     len2 = torch.from_numpy(np.array([3988] * nd + [486977], dtype=np.int32)).to(dev)
-    res["sst_file_desc_us"] = timed(lambda: crc32c.batch(buf, off2, len2, out=out))
+    res["sst_file_desc_us"] = timed(lambda: crc32c.batch(buf, off2, len2, out=out, check_bounds=False))
     res["data_blocks_fixed_us"] = timed(lambda: crc32c.batch_fixed(buf, 3992, 3988, nd, out=out[:nd]))
     bytes_ = nd * 3988
     res["data_bytes"] = bytes_

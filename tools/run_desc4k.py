@@ -18,7 +18,7 @@ def main():
     lens = torch.full((n,), 4096, dtype=torch.int32, device=dev)
     out = torch.empty(n, dtype=torch.int32, device=dev)
     for _ in range(int(sys.argv[1]) if len(sys.argv) > 1 else 3):
-        crc32c.batch(buf, off, lens, out=out)
+        crc32c.batch(buf, off, lens, out=out, check_bounds=False)
     torch.cuda.synchronize()
 
 

@@ -28,7 +28,7 @@ def main():
     ln = torch.from_numpy(np.tile(hlen.astype(np.int32) + 1, nf)).to(dev)
     crc32c.batch(buf, off, ln, mask=True, trailer=True, log_header=True)  # seal the headers
     for _ in range(int(sys.argv[1]) if len(sys.argv) > 1 else 3):
-        crc32c.batch(buf, off, ln, verify=True, log_header=True)
+        crc32c.batch(buf, off, ln, verify=True, log_header=True, check_bounds=False)
     torch.cuda.synchronize()
     print("records", off.numel())
 
