@@ -57,6 +57,11 @@ DeviceCtx g_ctx[kMaxDevices];
 // Test hook: route fixed-stride batches through the generic span kernel.
 bool g_force_generic = false;
 
+// Which descriptor batches go through the quad kernel first (spans of
+// <= kQuadMaxLen bytes; longer ones follow on the generic path):
+// 0 = log-record batches (PRISMDB_CRC32C_LOG_HEADER), 1 = all, -1 = none.
+int g_quad_mode = 0;
+
 void BuildTables(DeviceTables* t) {
   namespace g = prismdb::gf2;
   g::StrideTables(prismdb::dev::kStrideBytes, t->stride);
@@ -150,6 +155,7 @@ void InitDevice(DeviceCtx& ctx, int device) {
     return;
   }
   DeviceTables* host = new DeviceTables;
+  std::memset(host, 0, sizeof(DeviceTables));
   BuildTables(host);
   e = hipMalloc(&ctx.tabs, sizeof(DeviceTables));
   if (e == hipSuccess) e = hipMemcpy(ctx.tabs, host, sizeof(DeviceTables), hipMemcpyHostToDevice);
@@ -186,6 +192,8 @@ struct Workspace {
   void* mem = nullptr;
   char* grow = nullptr;
   size_t cap_rec = 0;
+  char* qgrow = nullptr;  // quad path: long-span list and its results, 9 B per span
+  size_t cap_q = 0;
   SplitWs ws{};
 };
 
@@ -197,7 +205,7 @@ size_t SliceCap(size_t n, uint32_t streams) { return n / 2 + 32 * (size_t)stream
 constexpr uint64_t kCapSeg = 1u << 20;   // 1 Mi segments = 32 GiB of long spans per call
 constexpr uint32_t kCapLong = 1u << 18;
 
-int GetWorkspace(hipStream_t s, size_t nspans, uint32_t streams, SplitWs* out) {
+int GetWorkspace(hipStream_t s, size_t nspans, uint32_t streams, bool quad, SplitWs* out) {
   thread_local std::map<std::pair<int, hipStream_t>, Workspace> cache;
   int device = 0;
   hipGetDevice(&device);
@@ -240,6 +248,21 @@ int GetWorkspace(hipStream_t s, size_t nspans, uint32_t streams, SplitWs* out) {
     if (e != hipSuccess) return FailHip(e, "span record workspace hipMalloc");
     w.cap_rec = cap;
   }
+  if (quad && w.cap_q < nspans) {
+    if (w.qgrow != nullptr) {
+      hipStreamSynchronize(s);
+      hipFree(w.qgrow);
+      w.qgrow = nullptr;
+      w.cap_q = 0;
+    }
+    const size_t cap = nspans < 4096 ? 4096 : nspans + nspans / 4;
+    hipError_t e = hipMalloc(reinterpret_cast<void**>(&w.qgrow), cap * 9 + 16);
+    if (e != hipSuccess) return FailHip(e, "quad list workspace hipMalloc");
+    w.cap_q = cap;
+  }
+  w.ws.list = quad ? reinterpret_cast<uint32_t*>(w.qgrow) : nullptr;
+  w.ws.qout = quad ? reinterpret_cast<uint32_t*>(w.qgrow + w.cap_q * 4) : nullptr;
+  w.ws.qmm = quad ? reinterpret_cast<uint8_t*>(w.qgrow + w.cap_q * 8) : nullptr;
   w.ws.rec = reinterpret_cast<prismdb::dev::SpanRec*>(w.grow);
   w.ws.slice_start = reinterpret_cast<uint64_t*>(w.grow + w.cap_rec * 16);
   w.ws.cnt = reinterpret_cast<uint32_t*>(w.grow + w.cap_rec * 16 + SliceCap(w.cap_rec, streams) * 8);
@@ -293,10 +316,23 @@ int RunBatch(DeviceCtx& ctx, const SpanBatch& base_args, bool desc, bool verify,
   SplitWs ws{};
   // The span kernel's record streams: two per wave of its persistent grid.
   const uint32_t streams = 2u * (uint32_t)ctx.cus * prismdb::dev::kWavesPerGroup;
-  int rc = GetWorkspace(s, a.n, streams, &ws);
+  // Short spans first, four per wave (crc32c_quad_kernel); the generic path
+  // below then runs over the list of the longer ones only.
+  const bool quad = desc && (g_quad_mode > 0 || (g_quad_mode == 0 && (a.flags & prismdb::dev::kFlagLogHeader)));
+  int rc = GetWorkspace(s, a.n, streams, quad, &ws);
   if (rc != 0) return rc;
   hipError_t e = hipMemsetAsync(ws.counters, 0, sizeof(SplitCounters), s);
   if (e != hipSuccess) return FailHip(e, "hipMemsetAsync");
+  uint32_t* const caller_out = a.out;
+  uint8_t* const caller_mm = a.mismatch;
+  if (quad) {
+    e = prismdb::dev::launch_quad(a, verify, ctx.cus, ws, s);
+    if (e != hipSuccess) return FailHip(e, "quad kernel launch");
+    a.idx = ws.list;
+    a.n_dev = &ws.counters->nlist;
+    if (a.out != nullptr) a.out = ws.qout;
+    if (a.mismatch != nullptr) a.mismatch = ws.qmm;
+  }
   a.skip_above = prismdb::dev::kLongSpan;
   // span records for the kernel launch_span picks (its chunk size)
   a.chunk_lg = (a.flags & prismdb::dev::kFlagLogHeader) ? prismdb::dev::kLgChunkWordsLog : 10u;
@@ -328,7 +364,15 @@ int RunBatch(DeviceCtx& ctx, const SpanBatch& base_args, bool desc, bool verify,
   e = prismdb::dev::launch_span(seg, false, ctx.cus, s);
   if (e != hipSuccess) return FailHip(e, "segment kernel launch");
   e = prismdb::dev::launch_combine(a, desc, verify, ws, s);
-  return e == hipSuccess ? 0 : FailHip(e, "combine kernel launch");
+  if (e != hipSuccess) return FailHip(e, "combine kernel launch");
+  if (quad) {
+    SpanBatch back = a;
+    back.out = caller_out;
+    back.mismatch = caller_mm;
+    e = prismdb::dev::launch_scatter(back, ws, ws.qout, ws.qmm, s);
+    if (e != hipSuccess) return FailHip(e, "scatter kernel launch");
+  }
+  return 0;
 }
 
 }  // namespace
@@ -407,5 +451,10 @@ const char* leveldb_crc32c_last_error(void) { return t_last_error.c_str(); }
 
 // Not in the public header: lets the parity tests pin the generic kernel too.
 void prismdb_crc32c_force_generic(int on) { g_force_generic = on != 0; }
+
+// Not in the public header: which descriptor batches take the quad kernel
+// (0 = log-record batches, the default; 1 = every batch; -1 = none), so the
+// parity tests and the A/B harness can pin either path.
+void prismdb_crc32c_quad_mode(int mode) { g_quad_mode = mode > 0 ? 1 : (mode < 0 ? -1 : 0); }
 
 }  // extern "C"

@@ -44,7 +44,15 @@ struct DeviceTables {
   uint32_t shift_seg[32];     // column i of shift_kSegment (M)
   uint32_t shift_seg64[32];   // column i of M^64
   uint32_t lane_seg[32][64];  // [i][l] = column i of M^(63-l): lane l's final shift
+  uint32_t zero[4];           // 16 zero bytes: the quad kernel's loads of unused lanes land here
 };
+
+// Short-record ("quad") kernel: spans of len <= kQuadMaxLen, four per wave,
+// each on one 16-lane DPP row with four 256-B-stride sub-streams per lane
+// (crc32c_kernels.hip).  A frame is kQuadRounds rounds of 64 words.
+constexpr int kQuadRounds = 5;
+constexpr uint32_t kQuadWords = 64u * kQuadRounds;   // 320 body words
+constexpr uint32_t kQuadMaxLen = 4u * kQuadWords;    // len <= 1280 B => <= 320 body words
 
 enum : uint32_t { kRoleSpans = 0, kRoleSegments = 1 };
 
@@ -75,6 +83,10 @@ struct SpanBatch {
   const uint64_t* slice_start;
   const unsigned long long* nslices_dev;
   uint32_t chunk_lg;  // planner: log2(chunk words) of the kernel that consumes the span records
+  // nullable: record i of this batch is span idx[i] of the caller's
+  // descriptors and results (the generic path behind the quad kernel runs
+  // over the list of spans too long for it; n_dev holds the list length)
+  const uint32_t* idx;
 };
 
 struct SplitCounters {
@@ -84,6 +96,7 @@ struct SplitCounters {
   unsigned long long tasks;    // chunk tasks of the span pass (long spans count 1)
   unsigned long long nslices;  // slices of 2^lg_tau tasks
   uint32_t lg_tau;
+  unsigned long long nlist;    // spans the quad kernel leaves to the generic path
 };
 
 struct SplitWs {
@@ -103,6 +116,9 @@ struct SplitWs {
   uint64_t tile;          // records per planner block
   uint32_t nblocks;       // planner blocks (<= kMaxPlanBlocks)
   uint32_t nstreams;      // span-kernel record streams (2 per wave)
+  uint32_t* list;         // quad path: indices of the spans longer than kQuadMaxLen
+  uint32_t* qout;         // quad path: generic-path results of the listed spans (list order)
+  uint8_t* qmm;
 };
 
 constexpr uint32_t kMaxPlanBlocks = 4096;
@@ -114,6 +130,9 @@ hipError_t launch_fixed(const SpanBatch& a, bool verify, int grid, hipStream_t s
 hipError_t launch_plan(const SpanBatch& a, bool desc, const SplitWs& ws, hipStream_t s);
 hipError_t launch_slices(const SpanBatch& a, const SplitWs& ws, hipStream_t s);
 hipError_t launch_combine(const SpanBatch& a, bool desc, bool verify, const SplitWs& ws,
+                          hipStream_t s);
+hipError_t launch_quad(const SpanBatch& a, bool verify, int grid, const SplitWs& ws, hipStream_t s);
+hipError_t launch_scatter(const SpanBatch& a, const SplitWs& ws, const uint32_t* qout, const uint8_t* qmm,
                           hipStream_t s);
 
 }  // namespace dev

@@ -68,6 +68,9 @@
 #ifndef PRISMDB_LOG_ROUNDSKIP  // log-record kernel: skip chunk 0's padding rounds
 #define PRISMDB_LOG_ROUNDSKIP 1
 #endif
+#ifndef PRISMDB_QUAD_RING
+#define PRISMDB_QUAD_RING 2  // tasks in the quad kernel's ring (one folded, the rest in flight)
+#endif
 #ifndef PRISMDB_RUN_LG
 #define PRISMDB_RUN_LG 5  // fixed kernel: log2(pair steps per run); runs of 2 << PRISMDB_RUN_LG spans
 #endif
@@ -923,9 +926,20 @@ __global__ __launch_bounds__(kThreads) void crc32c_fixed_kernel(SpanBatch a) {
 // own record for the segment pass.  Block b covers records [b*tile, +tile) and
 // leaves its task sum in bsum[b] for the slice scan.
 // ---------------------------------------------------------------------------
+// Records of the batch: n, or the device count when the batch is the quad
+// kernel's list of long spans.
+__device__ __forceinline__ uint64_t batch_n(const SpanBatch& a) {
+  uint64_t n = a.n;
+  if (a.n_dev != nullptr) {
+    const uint64_t m = *a.n_dev;
+    n = m < n ? m : n;
+  }
+  return n;
+}
+
 template <bool kDesc>
 __global__ __launch_bounds__(kPlanThreads) void crc32c_plan_kernel(SpanBatch a, SplitWs ws) {
-  const uint64_t n = a.n;
+  const uint64_t n = batch_n(a);
   const uint64_t lo = (uint64_t)blockIdx.x * ws.tile;
   const uint64_t hi = lo + ws.tile < n ? lo + ws.tile : n;
   __shared__ unsigned long long sum;
@@ -933,9 +947,10 @@ __global__ __launch_bounds__(kPlanThreads) void crc32c_plan_kernel(SpanBatch a, 
   __syncthreads();
   uint32_t mine = 0;  // <= tile/256 spans of <= 32 tasks each
   for (uint64_t i = lo + threadIdx.x; i < hi; i += kPlanThreads) {
-    const uint64_t off = kDesc ? a.off[i] : i * a.stride;
-    const uint32_t len = kDesc ? a.len[i] : a.len_c;
-    const uint32_t init = kDesc ? (a.init != nullptr ? a.init[i] : 0u) : a.init_c;
+    const uint64_t q = a.idx != nullptr ? a.idx[i] : i;  // the caller's span
+    const uint64_t off = kDesc ? a.off[q] : q * a.stride;
+    const uint32_t len = kDesc ? a.len[q] : a.len_c;
+    const uint32_t init = kDesc ? (a.init != nullptr ? a.init[q] : 0u) : a.init_c;
     const uint8_t* p = a.base + off;
     const bool lng = len > a.skip_above;
     const SpanRec r = make_rec(p, len, init, lng, a.chunk_lg);
@@ -1023,9 +1038,10 @@ __global__ __launch_bounds__(1024) void crc32c_slice_scan_kernel(SpanBatch a, Sp
     // Every span one task (4 KiB blocks, log records, SST data blocks): slices
     // of tau tasks are runs of tau records, which the span kernel deals
     // without slice starts -- nslices = 0 says so and the mark pass is skipped.
-    ws.counters->nslices = T == a.n ? 0 : K;
+    const uint64_t n = batch_n(a);
+    ws.counters->nslices = T == n ? 0 : K;
     ws.slice_start[0] = 0;
-    ws.slice_start[K] = a.n;
+    ws.slice_start[K] = n;
   }
 }
 
@@ -1033,7 +1049,7 @@ __global__ __launch_bounds__(kPlanThreads) void crc32c_slice_mark_kernel(SpanBat
   const uint64_t K = ws.counters->nslices;
   if (K == 0) return;  // uniform batch: runs, no slice starts
   __shared__ uint64_t sh[kPlanThreads];
-  const uint64_t n = a.n;
+  const uint64_t n = batch_n(a);
   const uint32_t lg = ws.counters->lg_tau;
   // Thread t walks its own per = tile/256 consecutive records of the block's
   // tile: one block scan per tile instead of one per 256 records.
@@ -1097,8 +1113,9 @@ __global__ __launch_bounds__(256) void crc32c_combine_kernel(SpanBatch a, SplitW
     const uint32_t crc = y ^ kConditioning;
     const uint32_t res = (a.flags & kFlagMask) ? mask_crc(crc) : crc;
     if (a.out != nullptr) a.out[span] = res;
-    const uint64_t off = kDesc ? a.off[span] : span * a.stride;
-    const uint32_t len = kDesc ? a.len[span] : a.len_c;
+    const uint64_t q = a.idx != nullptr ? a.idx[span] : span;  // the caller's span
+    const uint64_t off = kDesc ? a.off[q] : q * a.stride;
+    const uint32_t len = kDesc ? a.len[q] : a.len_c;
     const bool hdr = (a.flags & kFlagLogHeader) != 0;
     const uint8_t* t = hdr ? a.base + off - kLogCrcBack : a.base + off + len;
     if (a.flags & kFlagWriteTrailer) store_le32(t, res);
@@ -1107,6 +1124,386 @@ __global__ __launch_bounds__(256) void crc32c_combine_kernel(SpanBatch a, SplitW
                               ((uint32_t)t[3] << 24);
       a.mismatch[span] = crc != unmask_crc(stored) ? 1 : 0;
     }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Short records: the quad kernel (spans of len <= kQuadMaxLen, <= 320 body
+// words: log records, small blocks).  The span kernel spends one wave-wide
+// fold, realignment, reduction and ~190 scalar instructions per ~1 KB record
+// (profiles/r01_wal_pmc); here a wave takes FOUR records at a time:
+//   * DPP row g = lane >> 4 (16 lanes) takes record 4q + g of the wave's run
+//     of 64 consecutive records (runs dealt round-robin to the waves);
+//   * lane j of the row runs four 256-B-stride sub-streams k = 0..3: virtual
+//     lane v = 16 (k ^ (g & 1)) + j of a 64-lane frame.  So the stride
+//     tables, the fold and lane v's realignment tables are the other
+//     kernels' (odd rows take their sub-streams in swapped pairs: the
+//     realignment lookups of rows 0/1 and 2/3 then hit different banks);
+//   * a frame is kQuadRounds rounds of 64 words with the record's body
+//     right-aligned (word i at frame position P + i, P = 320 - W), loaded
+//     with one dword per sub-stream and round: 20 loads per lane per task,
+//     addresses clamped into the record; the positions before P are zeroed
+//     at fold time, where the register after the head bytes enters with
+//     body word 0 (position P).  Rounds before the task's longest record are
+//     not folded;
+//   * head bytes, tail bytes and the stored crc ride in one byte load per
+//     lane (quads 0, 1, 2 of the row) and are fed with 16-lane GF(2)
+//     products: shift_t is a 32x32 matrix, lane j holds columns 2j, 2j+1;
+//   * the row's CRC is one DPP row reduction; lane i of the run collects
+//     record i's result (ds_bpermute) for one coalesced store per run.
+// Per record that is one scalar descriptor read and a quarter of the fold's
+// fixed costs.  Spans longer than kQuadMaxLen are left to the generic path
+// (crc32c_long_list_kernel lists them); this kernel stores a placeholder for
+// them that the scatter pass overwrites.
+// ---------------------------------------------------------------------------
+
+// Columns 2j and 2j+1 of shift_1, shift_2, shift_3 for the row products.
+struct RowShift {
+  uint32_t c[3][2];
+};
+
+__device__ __forceinline__ RowShift row_shift_cols(uint32_t j) {
+  RowShift s;
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    uint32_t c = 1u << (2u * j + (uint32_t)b);
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) c = (c >> 1) ^ (kPolyReflected & (0u - (c & 1u)));
+      s.c[t][b] = c;
+    }
+  }
+  return s;
+}
+
+// shift_t(x), t = 0..3, for x and t uniform within each 16-lane row (every
+// lane of the row gets the product).
+__device__ __forceinline__ uint32_t row_shift(const RowShift& s, uint32_t j, uint32_t x, uint32_t t) {
+  // selected with masks: a ternary chain here compiles to an indexed (scratch) array
+  const uint32_t m1 = t == 1u ? ~0u : 0u, m2 = t == 2u ? ~0u : 0u, m3 = t == 3u ? ~0u : 0u;
+  const uint32_t c0 = (s.c[0][0] & m1) | (s.c[1][0] & m2) | (s.c[2][0] & m3);
+  const uint32_t c1 = (s.c[0][1] & m1) | (s.c[1][1] & m2) | (s.c[2][1] & m3);
+  const uint32_t b = x >> (2u * j);
+  const uint32_t y = row_xor(((b & 1u) ? c0 : 0u) ^ ((b & 2u) ? c1 : 0u));
+  return t ? y : x;
+}
+
+// Lane n of the row, broadcast to the row (DPP row_newbcast).
+template <int kN>
+__device__ __forceinline__ uint32_t row_bcast(uint32_t v) {
+  return __builtin_amdgcn_update_dpp(0u, v, 0x150 + kN, 0xF, 0xF, false);
+}
+
+// Inline-asm loads at a per-task scalar base + 32-bit per-lane offset;
+// retired by wait_quad.
+__device__ __forceinline__ uint32_t asm_load_dword_s(const uint8_t* sbase, uint32_t voff) {
+  uint32_t r;
+#if PRISMDB_NT_LOADS
+  asm volatile("global_load_dword %0, %1, %2 nt" : "=v"(r) : "v"(voff), "s"(sbase));
+#else
+  asm volatile("global_load_dword %0, %1, %2" : "=v"(r) : "v"(voff), "s"(sbase));
+#endif
+  return r;
+}
+
+__device__ __forceinline__ uint32_t asm_load_ubyte_s(const uint8_t* sbase, uint32_t voff) {
+  uint32_t r;
+  asm volatile("global_load_ubyte %0, %1, %2" : "=v"(r) : "v"(voff), "s"(sbase));
+  return r;
+}
+
+// Wait for one task's 20 body words and its edge byte with kYounger loads
+// (the younger tasks) left in flight; the registers are in/out operands so no
+// consumer is scheduled above the wait.
+template <int kYounger>
+__device__ __forceinline__ void wait_quad(uint32_t (&w)[kQuadRounds][4], uint32_t& e) {
+  static_assert(kQuadRounds == 5, "20 body words per task");
+  asm volatile("s_waitcnt vmcnt(%21)"
+               : "+v"(w[0][0]), "+v"(w[0][1]), "+v"(w[0][2]), "+v"(w[0][3]), "+v"(w[1][0]), "+v"(w[1][1]),
+                 "+v"(w[1][2]), "+v"(w[1][3]), "+v"(w[2][0]), "+v"(w[2][1]), "+v"(w[2][2]), "+v"(w[2][3]),
+                 "+v"(w[3][0]), "+v"(w[3][1]), "+v"(w[3][2]), "+v"(w[3][3]), "+v"(w[4][0]), "+v"(w[4][1]),
+                 "+v"(w[4][2]), "+v"(w[4][3]), "+v"(e)
+               : "n"(kYounger)
+               : "memory");
+}
+
+// A task's window.  Its four records (4-aligned indices tb .. tb+3, those
+// below n) are read through one scalar base: rows whose bytes (with the log
+// header before or the trailer after) lie within 2 GiB of the lowest short
+// record are the quad kernel's; a short record outside that window is listed
+// for the generic path like a long one.  The list kernel and the quad kernel
+// evaluate this same function.
+struct QuadWindow {
+  uint64_t lo;    // lowest offset among the short records (valid if any)
+  uint32_t mask;  // bit q: record tb + q is the quad kernel's
+};
+
+__device__ __forceinline__ QuadWindow quad_window(const uint64_t (&off)[4], const uint32_t (&len)[4],
+                                                  uint32_t valid) {
+  QuadWindow w{~0ull, 0u};
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    if (((valid >> q) & 1u) && len[q] <= kQuadMaxLen && off[q] < w.lo) w.lo = off[q];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    if (((valid >> q) & 1u) && len[q] <= kQuadMaxLen && off[q] - w.lo + len[q] + 16u < (1ull << 31))
+      w.mask |= 1u << q;
+  return w;
+}
+
+// Wave-uniform task: records tb .. tb+3, the scalar base and the fold bounds.
+struct QuadTask {
+  uint64_t tb;
+  const uint8_t* sbase;
+  uint32_t u;  // m0 | mp << 4 | any head << 8 | any tail << 9 | any bodyless record << 10
+};
+constexpr uint32_t kQuadAnyH = 1u << 8, kQuadAnyT = 1u << 9, kQuadAnyW0 = 1u << 10;
+
+template <bool kVerify>
+__global__ __launch_bounds__(kThreads) void crc32c_quad_kernel(SpanBatch a) {
+  const uint64_t n = a.n;
+  __shared__ uint32_t lds[kLdsWords];
+  const uint32_t tid = threadIdx.x;
+  load_tables(lds, a.tabs, tid);
+  const uint32_t lane = tid & 63u, g = lane >> 4, j = lane & 15u;
+  __syncthreads();
+  const StrideLanes tab = stride_lanes(lane);
+  const RowShift rsh = row_shift_cols(j);
+  // sub-stream k = virtual lane 16 (k ^ (g & 1)) + j; its realignment entry
+  uint32_t nib[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) nib[k] = 4u * ((uint32_t)kTabWords + 16u * ((uint32_t)k ^ (g & 1u)) + j);
+  auto vlane = [&](int k) -> uint32_t { return (nib[k] >> 2) - (uint32_t)kTabWords; };
+  const uint64_t wave = rfl(blockIdx.x * kWavesPerGroup + (tid >> 6));
+  const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerGroup;
+  // Runs of 64 records (16 tasks), run r of wave w = records [(r nwaves + w) 64, +64).
+  const uint64_t jump = (nwaves - 1u) * 64u + 4u;
+  auto adv = [&](uint64_t tb) -> uint64_t { return ((tb + 4u) & 63u) ? tb + 4u : tb + jump; };
+  uint64_t cur = wave * 64u;
+  if (cur >= n) return;
+  const bool hdr = (a.flags & kFlagLogHeader) != 0;
+  const uint8_t* const zero = reinterpret_cast<const uint8_t*>(&a.tabs->zero[0]);
+
+  // Issue task tb: descriptors (scalar), the lane's row geometry, 21 loads.
+  // vmeta = W | P << 9 | h << 18 | t << 20 | ok << 22 | edge-byte-used << 23;
+  // vr0 = init ^ ~0; vpo = offset of the record's first byte from sbase.
+  auto issue = [&](uint64_t tb, uint32_t (&w)[kQuadRounds][4], uint32_t& e, QuadTask& tk, uint32_t& vmeta,
+                   uint32_t& vr0, uint32_t& vpo) {
+    uint64_t off[4];
+    uint32_t len[4], valid = 0u;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint64_t i = tb + (uint64_t)q;
+      const uint64_t ic = i < n ? i : n - 1u;
+      off[q] = const_load(a.off, ic);
+      len[q] = const_load(a.len, ic);
+      valid |= (i < n ? 1u : 0u) << q;
+    }
+    const QuadWindow win = quad_window(off, len, valid);
+    // base 8 bytes below the lowest record: every offset below is >= 2
+    tk.sbase = win.mask ? a.base + win.lo - 8u : zero;
+    tk.tb = tb;
+    uint32_t rmax = 0u, mp = 0u, any = 0u;
+    vmeta = 0u;
+    vr0 = 0u;
+    vpo = 0u;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const bool ok = (win.mask >> q) & 1u;
+      const uint32_t ln = len[q];
+      uint32_t h = (0u - (uint32_t)(reinterpret_cast<uintptr_t>(a.base) + off[q])) & 3u;
+      h = h < ln ? h : ln;
+      uint32_t W = (ln - h) >> 2, t = (ln - h) & 3u;
+      if (!ok) W = h = t = 0u;
+      const uint32_t P = kQuadWords - W;
+      const uint32_t R = (W + 63u) >> 6;
+      rmax = R > rmax ? R : rmax;
+      // rows without body words read someone else's bytes: all rounds masked
+      mp = (W ? P >> 6 : (uint32_t)kQuadRounds) > mp ? (W ? P >> 6 : (uint32_t)kQuadRounds) : mp;
+      any |= (h ? kQuadAnyH : 0u) | (t ? kQuadAnyT : 0u) | (ok && W == 0u ? kQuadAnyW0 : 0u);
+      const uint32_t ini = a.init != nullptr && ok ? const_load(a.init, tb + (uint64_t)q) : 0u;
+      const uint32_t po = ok ? (uint32_t)(off[q] - win.lo) + 8u : 8u;
+      if (g == (uint32_t)q) {
+        vmeta = W | (P << 9) | (h << 18) | (t << 20) | ((uint32_t)ok << 22);
+        vr0 = ini ^ kConditioning;
+        vpo = po;
+      }
+    }
+    tk.u = ((uint32_t)kQuadRounds - rmax) | (mp << 4) | any;
+    const uint32_t W = vmeta & 511u, P = (vmeta >> 9) & 511u, h = (vmeta >> 18) & 3u, t = (vmeta >> 20) & 3u;
+    const bool ok = (vmeta >> 22) & 1u;
+    // Body words: frame position 64 m + v is body word 64 m + v - P, clamped
+    // into the record (the fold zeroes the words outside it).
+    const uint32_t wm1 = W ? W - 1u : 0u;
+    const uint32_t bo = vpo + h;  // body offset
+#pragma unroll
+    for (int m = 0; m < kQuadRounds; ++m) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t idx = vlane(k) + 64u * (uint32_t)m - P;
+        w[m][k] = asm_load_dword_s(tk.sbase, bo + 4u * (idx < wm1 ? idx : wm1));
+      }
+    }
+    // Edge byte: quad 0 of the row loads head byte o (o < h), quad 1 tail
+    // byte o (o < t), quad 2 stored-crc byte o (verify); the rest are masked.
+    const uint32_t qd = j >> 2, o = j & 3u;
+    bool ev = false;
+    uint32_t eo = vpo;
+    if (qd == 0u) {
+      ev = o < h;
+      eo = vpo + o;
+    } else if (qd == 1u) {
+      ev = o < t;
+      eo = bo + 4u * W + o;
+    } else if (qd == 2u) {
+      ev = kVerify && ok;
+      eo = hdr ? vpo - kLogCrcBack + o : bo + 4u * W + t + o;
+    }
+    vmeta |= (ev ? 1u : 0u) << 23;
+    e = asm_load_ubyte_s(tk.sbase, ev ? eo : vpo);
+  };
+
+  uint32_t res = 0u, bad = 0u;
+  auto fold = [&](const QuadTask& tk, const uint32_t (&w)[kQuadRounds][4], uint32_t e, uint32_t vmeta,
+                  uint32_t vr0, uint32_t vpo) {
+    const uint32_t W = vmeta & 511u, P = (vmeta >> 9) & 511u, h = (vmeta >> 18) & 3u, t = (vmeta >> 20) & 3u;
+    const bool ok = (vmeta >> 22) & 1u;
+    const uint32_t m0 = tk.u & 15u, mp = (tk.u >> 4) & 15u;
+    // Edge words: each quad ORs its bytes (disjoint), rows broadcast quad 0
+    // (head), quad 1 (tail), quad 2 (stored crc).
+    uint32_t ew = ((vmeta >> 23) & 1u) ? e << (8u * (j & 3u)) : 0u;
+    ew = xor_dpp(xor_dpp(ew, 0xB1), 0x4E);
+    uint32_t r = vr0;  // register before the head bytes
+    if (tk.u & kQuadAnyH) r = row_shift(rsh, j, r ^ row_bcast<0>(ew), h);
+    uint32_t acc[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int m = 0; m < kQuadRounds; ++m) {
+      if ((uint32_t)m < m0) continue;
+      if ((uint32_t)m <= mp) {
+        // positions before the body read 0, body word 0 carries the register
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const uint32_t idx = vlane(k) + 64u * (uint32_t)m - P;
+          const uint32_t inj = idx == 0u ? r : 0u;
+          const uint32_t keep = idx < W ? ~0u : 0u;
+          acc[k] = step256(lds, tab, acc[k], __builtin_amdgcn_bitop3_b32(w[m][k], inj, keep, 0x28));
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) acc[k] = step256(lds, tab, acc[k], w[m][k]);
+      }
+    }
+    uint32_t x = xor3(realign(lds, nib[0], acc[0]), realign(lds, nib[1], acc[1]), realign(lds, nib[2], acc[2])) ^
+                 realign(lds, nib[3], acc[3]);
+    x = row_xor(x);
+    if (tk.u & kQuadAnyW0) x = W == 0u ? r : x;  // no body words: the register after the head
+    if (tk.u & kQuadAnyT) x = row_shift(rsh, j, x ^ row_bcast<4>(ew), t);
+    const uint32_t crc = x ^ kConditioning;
+    const uint32_t v = (a.flags & kFlagMask) ? mask_crc(crc) : crc;
+    if ((a.flags & kFlagWriteTrailer) && ok && j == 0u)
+      store_le32(tk.sbase + (hdr ? vpo - kLogCrcBack : vpo + h + 4u * W + t), v);
+    // Lane i of the run collects record i: task tir's rows go to lanes 4 tir .. 4 tir + 3.
+    const uint32_t tir = (uint32_t)(tk.tb >> 2) & 15u;
+    const int src = (int)((lane & 3u) << 6);  // byte address of lane 16 (lane & 3)
+    const bool mine = (lane >> 2) == tir;
+    const uint32_t gv = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)v);
+    res = mine ? gv : res;
+    if (kVerify) {
+      const uint32_t bd = crc != unmask_crc(row_bcast<8>(ew)) ? 1u : 0u;
+      const uint32_t gb = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)bd);
+      bad = mine ? gb : bad;
+    }
+    // Run end: one coalesced store of the run's results (placeholders for
+    // listed spans, rewritten by the scatter pass).
+    if (tir == 15u || tk.tb + 4u >= n) {
+      const uint64_t rb = tk.tb & ~63ull;
+      if (rb + lane < n) {
+        if (a.out != nullptr) __builtin_nontemporal_store(res, a.out + rb + lane);
+        if (kVerify && a.mismatch != nullptr) __builtin_nontemporal_store((uint8_t)bad, a.mismatch + rb + lane);
+      }
+    }
+  };
+
+  // Ring of kRing tasks, compile-time slots: fold one while the others are in flight.
+  constexpr int kRing = PRISMDB_QUAD_RING;
+  constexpr int kYounger = (kRing - 1) * (4 * kQuadRounds + 1);
+  static_assert(kYounger <= 63, "vmcnt is a 6-bit counter");
+  uint32_t wq[kRing][kQuadRounds][4];
+  uint32_t eq[kRing];
+  QuadTask tq[kRing];
+  uint32_t vm[kRing], vr[kRing], vp[kRing];
+  uint64_t ahead = cur;
+#pragma unroll
+  for (int d = 0; d < kRing; ++d) {
+    issue(ahead, wq[d], eq[d], tq[d], vm[d], vr[d], vp[d]);
+    ahead = adv(ahead);
+  }
+  for (;;) {
+#pragma unroll
+    for (int sl = 0; sl < kRing; ++sl) {
+      wait_quad<kYounger>(wq[sl], eq[sl]);
+      if (tq[sl].tb < n) fold(tq[sl], wq[sl], eq[sl], vm[sl], vr[sl], vp[sl]);
+      cur = adv(cur);
+      issue(ahead, wq[sl], eq[sl], tq[sl], vm[sl], vr[sl], vp[sl]);
+      ahead = adv(ahead);
+    }
+    if (cur >= n) break;
+  }
+  // Retire the tasks still in flight while their registers are live.
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int d = 0; d < kRing; ++d) {
+#pragma unroll
+    for (int m = 0; m < kQuadRounds; ++m) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) asm volatile("" : "+v"(wq[d][m][k]));
+    }
+    asm volatile("" : "+v"(eq[d]));
+  }
+}
+
+// The spans the quad kernel leaves to the generic path (len > kQuadMaxLen, or
+// outside their task's window), listed in runs of one wave's 64 consecutive
+// spans; ws.counters->nlist is the count.
+__global__ __launch_bounds__(256) void crc32c_long_list_kernel(SpanBatch a, SplitWs ws) {
+  const uint64_t n = a.n;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t step = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); b < n; b += step) {
+    const uint64_t i = b + lane;
+    // the task (4-aligned quad of records) this lane's record belongs to
+    const uint64_t t0 = i & ~3ull;
+    uint64_t off[4];
+    uint32_t len[4], valid = 0u;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint64_t r = t0 + (uint64_t)q;
+      const uint64_t rc = r < n ? r : n - 1u;
+      off[q] = a.off[rc];
+      len[q] = a.len[rc];
+      valid |= (r < n ? 1u : 0u) << q;
+    }
+    const QuadWindow win = quad_window(off, len, valid);
+    const bool lng = i < n && !((win.mask >> (i & 3u)) & 1u);
+    const uint64_t m = __ballot(lng);
+    if (m == 0) continue;
+    unsigned long long pos = 0;
+    if (lane == 0) pos = atomicAdd(&ws.counters->nlist, (unsigned long long)__popcll(m));
+    pos = __shfl(pos, 0);
+    if (lng) ws.list[pos + (uint64_t)__popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)i;
+  }
+}
+
+// Generic-path results of the listed spans, back to the caller's arrays.
+__global__ __launch_bounds__(256) void crc32c_scatter_kernel(SpanBatch a, SplitWs ws, const uint32_t* qout,
+                                                             const uint8_t* qmm) {
+  const uint64_t nl = ws.counters->nlist;
+  const uint64_t step = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nl; i += step) {
+    const uint32_t q = ws.list[i];
+    if (a.out != nullptr) a.out[q] = qout[i];
+    if (a.mismatch != nullptr) a.mismatch[q] = qmm[i];
   }
 }
 
@@ -1155,6 +1552,20 @@ hipError_t launch_plan(const SpanBatch& a, bool desc, const SplitWs& ws, hipStre
 hipError_t launch_slices(const SpanBatch& a, const SplitWs& ws, hipStream_t s) {
   crc32c_slice_scan_kernel<<<1, 1024, 0, s>>>(a, ws);
   crc32c_slice_mark_kernel<<<ws.nblocks, kPlanThreads, 0, s>>>(a, ws);
+  return hipGetLastError();
+}
+
+hipError_t launch_quad(const SpanBatch& a, bool verify, int grid, const SplitWs& ws, hipStream_t s) {
+  const int lgrid = (int)((a.n + 255u) / 256u < 2048u ? (a.n + 255u) / 256u : 2048u);
+  crc32c_long_list_kernel<<<lgrid, 256, 0, s>>>(a, ws);
+  if (verify) crc32c_quad_kernel<true><<<grid, kThreads, 0, s>>>(a);
+  else crc32c_quad_kernel<false><<<grid, kThreads, 0, s>>>(a);
+  return hipGetLastError();
+}
+
+hipError_t launch_scatter(const SpanBatch& a, const SplitWs& ws, const uint32_t* qout, const uint8_t* qmm,
+                          hipStream_t s) {
+  crc32c_scatter_kernel<<<256, 256, 0, s>>>(a, ws, qout, qmm);
   return hipGetLastError();
 }
 

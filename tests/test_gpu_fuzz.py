@@ -1,7 +1,9 @@
 """Randomized parity of the batch engine against the oracle: random span
 geometries (empty to split-path lengths, any alignment, overlapping), random
 flags (MASK, verify, WRITE_TRAILER, LOG_HEADER) and random fixed-stride
-shapes, on the fast and on the generic kernel.  Bit-exact.
+shapes, on the fast and on the generic kernel, and descriptor batches with
+the short-record (quad) kernel in front of the generic path for every batch,
+for log batches only (the default) and for none.  Bit-exact.
 
 Expected values come from the oracle (oracle/crc32c_oracle.c, pinned to the
 reference's golden vectors) on the same bytes; what a flag adds is checked
@@ -29,6 +31,17 @@ def dev(native):
     return torch.device("cuda", 0)
 
 
+@pytest.fixture(params=[0, 1, -1], ids=["quad_log", "quad_all", "quad_off"])
+def quad_mode(request, native):
+    """prismdb_crc32c_quad_mode: which descriptor batches take the quad kernel."""
+    import ctypes
+
+    native.prismdb_crc32c_quad_mode.argtypes = [ctypes.c_int]
+    native.prismdb_crc32c_quad_mode(request.param)
+    yield request.param
+    native.prismdb_crc32c_quad_mode(0)
+
+
 def _u32(t):
     return t.cpu().numpy().view(np.uint32)
 
@@ -48,7 +61,7 @@ def _lengths(rng, n):
 
 
 @pytest.mark.parametrize("seed", SEEDS)
-def test_random_spans(dev, oracle, seed):
+def test_random_spans(dev, oracle, quad_mode, seed):
     import torch
     from prismdb_amd import crc32c
 
@@ -84,7 +97,7 @@ def test_random_spans(dev, oracle, seed):
 
 
 @pytest.mark.parametrize("seed", SEEDS[:12])
-def test_random_trailer_sealing(dev, oracle, seed):
+def test_random_trailer_sealing(dev, oracle, quad_mode, seed):
     """WRITE_TRAILER on disjoint spans (a trailer must not land in another
     span): every trailer is LE32(Mask(crc)) or the raw crc, per MASK; bytes
     outside the trailers are untouched; LOG_HEADER writes 6 bytes before."""

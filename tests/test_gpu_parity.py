@@ -556,3 +556,80 @@ def test_host_pipeline_failure_drains_ring(dev, oracle):
     got, _ = crc32c.batch_host(host, off, lens)
     want, _ = oracle.batch(host, off, lens)
     np.testing.assert_array_equal(got, want)
+
+
+@pytest.fixture()
+def quad_all(native):
+    """Every descriptor batch through the quad kernel (prismdb_crc32c_quad_mode(1))."""
+    import ctypes
+
+    native.prismdb_crc32c_quad_mode.argtypes = [ctypes.c_int]
+    native.prismdb_crc32c_quad_mode(1)
+    yield
+    native.prismdb_crc32c_quad_mode(0)
+
+
+@pytest.mark.parametrize("log_header", [False, True])
+def test_quad_short_records(dev, oracle, quad_all, log_header):
+    """The short-record kernel on every length 0..1280 at every alignment, the
+    lengths just above its limit (generic path), random init, verify with the
+    stored crc after the span or (log records) 6 bytes before it, one damaged
+    record in four; record counts that end mid-task and mid-run."""
+    import torch
+    from prismdb_amd import crc32c
+
+    rng = np.random.default_rng(0x5EED0020 + log_header)
+    lens = np.concatenate([np.arange(0, 1281), [1281, 1282, 1283, 1284, 2000, 4096, 5000, 70_000],
+                           rng.integers(0, 1281, size=3000)]).astype(np.uint64)
+    rng.shuffle(lens)
+    n = len(lens) - 3  # 4290: not a multiple of 4 or of 64
+    lens = lens[:n]
+    gaps = rng.integers(6, 30, size=n).astype(np.uint64)
+    off = np.cumsum(np.concatenate([[7], (lens + gaps)[:-1]])).astype(np.uint64)
+    host = oracle.synth(int(off[-1] + lens[-1]) + 64, 0x5EED0021)
+    init = rng.integers(0, 2**32, size=n, dtype=np.uint64).astype(np.uint32)
+    raw, _ = oracle.batch(host, off, lens, init)
+    pos = off.astype(np.int64) - 6 if log_header else (off + lens).astype(np.int64)
+    damaged = rng.random(n) < 0.25
+    for i in range(n):
+        c = oracle.mask(int(raw[i])) ^ (1 if damaged[i] else 0)
+        host[pos[i]:pos[i] + 4] = np.frombuffer(np.uint32(c).tobytes(), dtype=np.uint8)
+    want, _ = oracle.batch(host, off, lens, init, mask=True)
+    buf = torch.from_numpy(host).to(dev)
+    d_off = torch.from_numpy(off.astype(np.int64)).to(dev)
+    d_len = torch.from_numpy(lens.astype(np.uint32).view(np.int32)).to(dev)
+    d_init = torch.from_numpy(init.view(np.int32)).to(dev)
+    out, mm = crc32c.batch(buf, d_off, d_len, d_init, mask=True, verify=True, log_header=log_header)
+    np.testing.assert_array_equal(_u32(out), want)
+    np.testing.assert_array_equal(mm.cpu().numpy(), damaged.astype(np.uint8))
+    out2, _ = crc32c.batch(buf, d_off, d_len)  # no init, no mask, no verify
+    np.testing.assert_array_equal(_u32(out2), oracle.batch(host, off, lens)[0])
+
+
+def test_quad_task_window(dev, oracle, quad_all):
+    """Records of one four-record task more than 2 GiB apart: the ones outside
+    the task's window go to the generic path, the results are the same."""
+    import torch
+    from prismdb_amd import crc32c
+
+    far = (2 << 30) + (256 << 20)
+    buf = torch.empty(far + (4 << 20), dtype=torch.uint8, device=dev)
+    crc32c.fill_synthetic(buf[:4 << 20], 0x5EED0022)
+    crc32c.fill_synthetic(buf[far:], 0x5EED0023)
+    lo = buf[:4 << 20].cpu().numpy()
+    hi = buf[far:].cpu().numpy()
+    rng = np.random.default_rng(0x5EED0024)
+    n = 1000
+    lens = rng.integers(0, 1281, size=n).astype(np.uint64)
+    rel = rng.integers(8, (4 << 20) - 1300, size=n).astype(np.uint64)
+    side = rng.random(n) < 0.4  # in the far region
+    off = rel + np.where(side, np.uint64(far), np.uint64(0))
+    want = np.empty(n, dtype=np.uint32)
+    for region, sel in ((lo, ~side), (hi, side)):
+        want[sel] = oracle.batch(region, rel[sel], lens[sel])[0]
+    d_off = torch.from_numpy(off.astype(np.int64)).to(dev)
+    d_len = torch.from_numpy(lens.astype(np.uint32).view(np.int32)).to(dev)
+    out, _ = crc32c.batch(buf, d_off, d_len)
+    np.testing.assert_array_equal(_u32(out), want)
+    del buf
+    torch.cuda.empty_cache()
