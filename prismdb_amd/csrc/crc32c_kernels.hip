@@ -1207,9 +1207,9 @@ __device__ __forceinline__ uint32_t asm_load_dword_s(const uint8_t* sbase, uint3
   return r;
 }
 
-__device__ __forceinline__ uint32_t asm_load_ubyte_s(const uint8_t* sbase, uint32_t voff) {
+__device__ __forceinline__ uint32_t asm_load_ubyte_v(uint64_t addr) {
   uint32_t r;
-  asm volatile("global_load_ubyte %0, %1, %2" : "=v"(r) : "v"(voff), "s"(sbase));
+  asm volatile("global_load_ubyte %0, %1, off" : "=v"(r) : "v"(addr));
   return r;
 }
 
@@ -1229,40 +1229,52 @@ __device__ __forceinline__ void wait_quad(uint32_t (&w)[kQuadRounds][4], uint32_
 }
 
 // A task's window.  Its four records (4-aligned indices tb .. tb+3, those
-// below n) are read through one scalar base: rows whose bytes (with the log
-// header before or the trailer after) lie within 2 GiB of the lowest short
-// record are the quad kernel's; a short record outside that window is listed
-// for the generic path like a long one.  The list kernel and the quad kernel
-// evaluate this same function.
+// below n) are read through one scalar base sb: the first short record A
+// anchors it, sb = address(A) - 8 - min(2^30, address(A) - 8), and a short
+// record is the quad kernel's if every byte it touches (log header before,
+// trailer after) lies in [sb, sb + 2^31 - 2048); any other short record is
+// listed for the generic path like a long one.  Offsets from sb then fit 31
+// bits, so the kernel computes them in 32 bits.  The list kernel and the quad
+// kernel evaluate this same function.
 struct QuadWindow {
-  uint64_t lo;    // lowest offset among the short records (valid if any)
+  uint64_t sb;
   uint32_t mask;  // bit q: record tb + q is the quad kernel's
 };
 
-__device__ __forceinline__ QuadWindow quad_window(const uint64_t (&off)[4], const uint32_t (&len)[4],
-                                                  uint32_t valid) {
-  QuadWindow w{~0ull, 0u};
+__device__ __forceinline__ QuadWindow quad_window(const uint8_t* base, const uint64_t (&off)[4],
+                                                  const uint32_t (&len)[4], uint32_t valid) {
+  uint32_t sh = 0u;
 #pragma unroll
-  for (int q = 0; q < 4; ++q)
-    if (((valid >> q) & 1u) && len[q] <= kQuadMaxLen && off[q] < w.lo) w.lo = off[q];
+  for (int q = 0; q < 4; ++q) sh |= (((valid >> q) & 1u) && len[q] <= kQuadMaxLen ? 1u : 0u) << q;
+  QuadWindow w{0u, 0u};
+  if (sh == 0u) return w;
+  const int A = __builtin_ctz(sh);
+  uint64_t oa = off[0];
 #pragma unroll
-  for (int q = 0; q < 4; ++q)
-    if (((valid >> q) & 1u) && len[q] <= kQuadMaxLen && off[q] - w.lo + len[q] + 16u < (1ull << 31))
-      w.mask |= 1u << q;
+  for (int q = 1; q < 4; ++q) oa = A == q ? off[q] : oa;
+  const uint64_t aa = reinterpret_cast<uint64_t>(base) + oa - 8u;
+  w.sb = aa - (aa < (1ull << 30) ? aa : (1ull << 30));
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const uint64_t d = reinterpret_cast<uint64_t>(base) + off[q] - w.sb;  // >= 8 when in the window
+    if (((sh >> q) & 1u) && d >= 8u && d < (1ull << 31) - 2048u) w.mask |= 1u << q;
+  }
   return w;
 }
 
 // Wave-uniform task: records tb .. tb+3, the scalar base and the fold bounds.
 struct QuadTask {
-  uint64_t tb;
-  const uint8_t* sbase;
+  uint32_t tb;
+  const uint8_t* sbase;  // body-word loads: the window base, or `zero` when no row has body words
+  const uint8_t* sb;     // the window base (edge bytes, trailers)
   uint32_t u;  // m0 | mp << 4 | any head << 8 | any tail << 9 | any bodyless record << 10
 };
 constexpr uint32_t kQuadAnyH = 1u << 8, kQuadAnyT = 1u << 9, kQuadAnyW0 = 1u << 10;
 
 template <bool kVerify>
 __global__ __launch_bounds__(kThreads) void crc32c_quad_kernel(SpanBatch a) {
-  const uint64_t n = a.n;
+  // record indices in 32 bits: the host cuts batches at kMaxGenericSpans (2^30)
+  const uint32_t n = (uint32_t)a.n;
   __shared__ uint32_t lds[kLdsWords];
   const uint32_t tid = threadIdx.x;
   load_tables(lds, a.tabs, tid);
@@ -1275,74 +1287,103 @@ __global__ __launch_bounds__(kThreads) void crc32c_quad_kernel(SpanBatch a) {
 #pragma unroll
   for (int k = 0; k < 4; ++k) nib[k] = 4u * ((uint32_t)kTabWords + 16u * ((uint32_t)k ^ (g & 1u)) + j);
   auto vlane = [&](int k) -> uint32_t { return (nib[k] >> 2) - (uint32_t)kTabWords; };
-  const uint64_t wave = rfl(blockIdx.x * kWavesPerGroup + (tid >> 6));
-  const uint64_t nwaves = (uint64_t)gridDim.x * kWavesPerGroup;
+  const uint32_t wave = rfl(blockIdx.x * kWavesPerGroup + (tid >> 6));
+  const uint32_t nwaves = gridDim.x * kWavesPerGroup;
   // Runs of 64 records (16 tasks), run r of wave w = records [(r nwaves + w) 64, +64).
-  const uint64_t jump = (nwaves - 1u) * 64u + 4u;
-  auto adv = [&](uint64_t tb) -> uint64_t { return ((tb + 4u) & 63u) ? tb + 4u : tb + jump; };
-  uint64_t cur = wave * 64u;
+  // (tb < n + 64 nwaves always, far below 2^32.)
+  const uint32_t jump = (nwaves - 1u) * 64u + 4u;
+  auto adv = [&](uint32_t tb) -> uint32_t { return ((tb + 4u) & 63u) ? tb + 4u : tb + jump; };
+  uint32_t cur = wave * 64u;
   if (cur >= n) return;
   const bool hdr = (a.flags & kFlagLogHeader) != 0;
   const uint8_t* const zero = reinterpret_cast<const uint8_t*>(&a.tabs->zero[0]);
 
-  // Issue task tb: descriptors (scalar), the lane's row geometry, 21 loads.
+  // The lane's row's value out of four uniform ones.
+  auto sel = [&](uint32_t x0, uint32_t x1, uint32_t x2, uint32_t x3) -> uint32_t {
+    const uint32_t lo = (lane & 16u) ? x1 : x0, hi = (lane & 16u) ? x3 : x2;
+    return (lane & 32u) ? hi : lo;
+  };
+  // Issue task tb: descriptors (scalar), the lane's row geometry (vector),
+  // the fold bounds (four readlanes), 21 loads.
   // vmeta = W | P << 9 | h << 18 | t << 20 | ok << 22 | edge-byte-used << 23;
   // vr0 = init ^ ~0; vpo = offset of the record's first byte from sbase.
-  auto issue = [&](uint64_t tb, uint32_t (&w)[kQuadRounds][4], uint32_t& e, QuadTask& tk, uint32_t& vmeta,
+  auto issue = [&](uint32_t tb, uint32_t (&w)[kQuadRounds][4], uint32_t& e, QuadTask& tk, uint32_t& vmeta,
                    uint32_t& vr0, uint32_t& vpo) {
     uint64_t off[4];
-    uint32_t len[4], valid = 0u;
+    uint32_t len[4], ini[4] = {0u, 0u, 0u, 0u}, valid;
+    if (tb + 4u <= n) {  // one contiguous scalar read per array
+      valid = 15u;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const uint64_t i = tb + (uint64_t)q;
-      const uint64_t ic = i < n ? i : n - 1u;
-      off[q] = const_load(a.off, ic);
-      len[q] = const_load(a.len, ic);
-      valid |= (i < n ? 1u : 0u) << q;
-    }
-    const QuadWindow win = quad_window(off, len, valid);
-    // base 8 bytes below the lowest record: every offset below is >= 2
-    tk.sbase = win.mask ? a.base + win.lo - 8u : zero;
-    tk.tb = tb;
-    uint32_t rmax = 0u, mp = 0u, any = 0u;
-    vmeta = 0u;
-    vr0 = 0u;
-    vpo = 0u;
+      for (int q = 0; q < 4; ++q) {
+        off[q] = const_load(a.off + tb, (uint64_t)q);
+        len[q] = const_load(a.len + tb, (uint64_t)q);
+      }
+      if (a.init != nullptr) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const bool ok = (win.mask >> q) & 1u;
-      const uint32_t ln = len[q];
-      uint32_t h = (0u - (uint32_t)(reinterpret_cast<uintptr_t>(a.base) + off[q])) & 3u;
-      h = h < ln ? h : ln;
-      uint32_t W = (ln - h) >> 2, t = (ln - h) & 3u;
-      if (!ok) W = h = t = 0u;
-      const uint32_t P = kQuadWords - W;
-      const uint32_t R = (W + 63u) >> 6;
-      rmax = R > rmax ? R : rmax;
-      // rows without body words read someone else's bytes: all rounds masked
-      mp = (W ? P >> 6 : (uint32_t)kQuadRounds) > mp ? (W ? P >> 6 : (uint32_t)kQuadRounds) : mp;
-      any |= (h ? kQuadAnyH : 0u) | (t ? kQuadAnyT : 0u) | (ok && W == 0u ? kQuadAnyW0 : 0u);
-      const uint32_t ini = a.init != nullptr && ok ? const_load(a.init, tb + (uint64_t)q) : 0u;
-      const uint32_t po = ok ? (uint32_t)(off[q] - win.lo) + 8u : 8u;
-      if (g == (uint32_t)q) {
-        vmeta = W | (P << 9) | (h << 18) | (t << 20) | ((uint32_t)ok << 22);
-        vr0 = ini ^ kConditioning;
-        vpo = po;
+        for (int q = 0; q < 4; ++q) ini[q] = const_load(a.init + tb, (uint64_t)q);
+      }
+    } else {  // the batch's last task (or past it): clamped reads
+      const uint32_t last = n - 1u;
+      valid = 0u;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint32_t i = tb + (uint32_t)q < last ? tb + (uint32_t)q : last;
+        off[q] = const_load(a.off, i);
+        len[q] = const_load(a.len, i);
+        if (a.init != nullptr) ini[q] = const_load(a.init, i);
+        valid |= (tb + (uint32_t)q < n ? 1u : 0u) << q;
       }
     }
-    tk.u = ((uint32_t)kQuadRounds - rmax) | (mp << 4) | any;
-    const uint32_t W = vmeta & 511u, P = (vmeta >> 9) & 511u, h = (vmeta >> 18) & 3u, t = (vmeta >> 20) & 3u;
-    const bool ok = (vmeta >> 22) & 1u;
+    const QuadWindow win = quad_window(a.base, off, len, valid);
+    tk.tb = tb;
+    tk.sb = reinterpret_cast<const uint8_t*>(win.sb);
+    // the row's record in 32 bits: its offset from sbase fits 31 bits
+    const uint32_t base_sb = (uint32_t)reinterpret_cast<uint64_t>(a.base) - (uint32_t)win.sb;
+    const uint32_t ln = sel(len[0], len[1], len[2], len[3]);
+    const bool ok = (win.mask >> g) & 1u;
+    vpo = ok ? base_sb + sel((uint32_t)off[0], (uint32_t)off[1], (uint32_t)off[2], (uint32_t)off[3]) : 8u;
+    vr0 = sel(ini[0], ini[1], ini[2], ini[3]) ^ kConditioning;
+    // head bytes up to 4-B alignment of the absolute address
+    uint32_t h = (0u - ((uint32_t)win.sb + vpo)) & 3u;
+    h = h < ln ? h : ln;
+    uint32_t W = (ln - h) >> 2, t = (ln - h) & 3u;
+    if (!ok) W = h = t = 0u;
+    const uint32_t P = kQuadWords - W;
+    vmeta = W | (P << 9) | (h << 18) | (t << 20) | ((uint32_t)ok << 22);
+    // fold bounds: rounds from 5 - Rmax, masked through mp (rows without
+    // body words read someone else's bytes: all rounds masked); flags
+    const uint32_t R = (W + 63u) >> 6, mpv = W ? P >> 6 : (uint32_t)kQuadRounds;
+    const uint32_t pk = R | (mpv << 4) | (h ? kQuadAnyH : 0u) | (t ? kQuadAnyT : 0u) |
+                        (ok && W == 0u ? kQuadAnyW0 : 0u);
+    const uint32_t p0 = readlane(pk, 0), p1 = readlane(pk, 16), p2 = readlane(pk, 32), p3 = readlane(pk, 48);
+    const uint32_t rmax = max(max(p0 & 15u, p1 & 15u), max(p2 & 15u, p3 & 15u));
+    const uint32_t mp = max(max((p0 >> 4) & 15u, (p1 >> 4) & 15u), max((p2 >> 4) & 15u, (p3 >> 4) & 15u));
+    tk.u = ((uint32_t)kQuadRounds - rmax) | (mp << 4) | ((p0 | p1 | p2 | p3) & (kQuadAnyH | kQuadAnyT | kQuadAnyW0));
     // Body words: frame position 64 m + v is body word 64 m + v - P, clamped
-    // into the record (the fold zeroes the words outside it).
-    const uint32_t wm1 = W ? W - 1u : 0u;
+    // into the record (the fold zeroes the words outside it).  A row without
+    // body words reads the first body word of the first row that has some
+    // (every address read is inside a record), or the zero block if none has.
     const uint32_t bo = vpo + h;  // body offset
+    const uint32_t rows_w = ((p0 & 15u) ? 1u : 0u) | ((p1 & 15u) ? 2u : 0u) | ((p2 & 15u) ? 4u : 0u) |
+                            ((p3 & 15u) ? 8u : 0u);
+    tk.sbase = rows_w ? tk.sb : zero;
+    const uint32_t safe = rows_w ? readlane(bo, 16u * (uint32_t)__builtin_ctz(rows_w)) : 0u;
+    const uint32_t wm1 = W ? W - 1u : 0u;
+    const uint32_t bw = W ? bo : safe;
+    // sub-stream k's body index in round 0; opaque, so that hipcc does not
+    // hoist the 20 loop-invariant v + 64 m out of the task loop (20 VGPRs)
+    uint32_t i0[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      i0[k] = vlane(k) - P;
+      asm volatile("" : "+v"(i0[k]));
+    }
 #pragma unroll
     for (int m = 0; m < kQuadRounds; ++m) {
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        const uint32_t idx = vlane(k) + 64u * (uint32_t)m - P;
-        w[m][k] = asm_load_dword_s(tk.sbase, bo + 4u * (idx < wm1 ? idx : wm1));
+        const uint32_t idx = i0[k] + 64u * (uint32_t)m;
+        w[m][k] = asm_load_dword_s(tk.sbase, bw + 4u * (idx < wm1 ? idx : wm1));
       }
     }
     // Edge byte: quad 0 of the row loads head byte o (o < h), quad 1 tail
@@ -1361,7 +1402,8 @@ __global__ __launch_bounds__(kThreads) void crc32c_quad_kernel(SpanBatch a) {
       eo = hdr ? vpo - kLogCrcBack + o : bo + 4u * W + t + o;
     }
     vmeta |= (ev ? 1u : 0u) << 23;
-    e = asm_load_ubyte_s(tk.sbase, ev ? eo : vpo);
+    // 64-bit address: an unused lane reads the zero block, not a byte of the window
+    e = asm_load_ubyte_v(ev ? reinterpret_cast<uint64_t>(tk.sb) + eo : reinterpret_cast<uint64_t>(zero));
   };
 
   uint32_t res = 0u, bad = 0u;
@@ -1377,6 +1419,12 @@ __global__ __launch_bounds__(kThreads) void crc32c_quad_kernel(SpanBatch a) {
     uint32_t r = vr0;  // register before the head bytes
     if (tk.u & kQuadAnyH) r = row_shift(rsh, j, r ^ row_bcast<0>(ew), h);
     uint32_t acc[4] = {0u, 0u, 0u, 0u};
+    uint32_t i0[4];  // as in issue(): opaque per-task indices
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      i0[k] = vlane(k) - P;
+      asm volatile("" : "+v"(i0[k]));
+    }
 #pragma unroll
     for (int m = 0; m < kQuadRounds; ++m) {
       if ((uint32_t)m < m0) continue;
@@ -1384,7 +1432,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_quad_kernel(SpanBatch a) {
         // positions before the body read 0, body word 0 carries the register
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          const uint32_t idx = vlane(k) + 64u * (uint32_t)m - P;
+          const uint32_t idx = i0[k] + 64u * (uint32_t)m;
           const uint32_t inj = idx == 0u ? r : 0u;
           const uint32_t keep = idx < W ? ~0u : 0u;
           acc[k] = step256(lds, tab, acc[k], __builtin_amdgcn_bitop3_b32(w[m][k], inj, keep, 0x28));
@@ -1394,17 +1442,23 @@ __global__ __launch_bounds__(kThreads) void crc32c_quad_kernel(SpanBatch a) {
         for (int k = 0; k < 4; ++k) acc[k] = step256(lds, tab, acc[k], w[m][k]);
       }
     }
-    uint32_t x = xor3(realign(lds, nib[0], acc[0]), realign(lds, nib[1], acc[1]), realign(lds, nib[2], acc[2])) ^
-                 realign(lds, nib[3], acc[3]);
+    // one sub-stream's eight lookups at a time (the memory clobber keeps the
+    // next batch of LDS reads below): 32 in flight at once cost 24 spilled VGPRs
+    uint32_t x = realign(lds, nib[0], acc[0]);
+#pragma unroll
+    for (int k = 1; k < 4; ++k) {
+      asm volatile("" ::: "memory");
+      x ^= realign(lds, nib[k], acc[k]);
+    }
     x = row_xor(x);
     if (tk.u & kQuadAnyW0) x = W == 0u ? r : x;  // no body words: the register after the head
     if (tk.u & kQuadAnyT) x = row_shift(rsh, j, x ^ row_bcast<4>(ew), t);
     const uint32_t crc = x ^ kConditioning;
     const uint32_t v = (a.flags & kFlagMask) ? mask_crc(crc) : crc;
     if ((a.flags & kFlagWriteTrailer) && ok && j == 0u)
-      store_le32(tk.sbase + (hdr ? vpo - kLogCrcBack : vpo + h + 4u * W + t), v);
+      store_le32(tk.sb + (hdr ? vpo - kLogCrcBack : vpo + h + 4u * W + t), v);
     // Lane i of the run collects record i: task tir's rows go to lanes 4 tir .. 4 tir + 3.
-    const uint32_t tir = (uint32_t)(tk.tb >> 2) & 15u;
+    const uint32_t tir = (tk.tb >> 2) & 15u;
     const int src = (int)((lane & 3u) << 6);  // byte address of lane 16 (lane & 3)
     const bool mine = (lane >> 2) == tir;
     const uint32_t gv = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)v);
@@ -1417,7 +1471,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_quad_kernel(SpanBatch a) {
     // Run end: one coalesced store of the run's results (placeholders for
     // listed spans, rewritten by the scatter pass).
     if (tir == 15u || tk.tb + 4u >= n) {
-      const uint64_t rb = tk.tb & ~63ull;
+      const uint32_t rb = tk.tb & ~63u;
       if (rb + lane < n) {
         if (a.out != nullptr) __builtin_nontemporal_store(res, a.out + rb + lane);
         if (kVerify && a.mismatch != nullptr) __builtin_nontemporal_store((uint8_t)bad, a.mismatch + rb + lane);
@@ -1433,7 +1487,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_quad_kernel(SpanBatch a) {
   uint32_t eq[kRing];
   QuadTask tq[kRing];
   uint32_t vm[kRing], vr[kRing], vp[kRing];
-  uint64_t ahead = cur;
+  uint32_t ahead = cur;
 #pragma unroll
   for (int d = 0; d < kRing; ++d) {
     issue(ahead, wq[d], eq[d], tq[d], vm[d], vr[d], vp[d]);
@@ -1484,7 +1538,7 @@ __global__ __launch_bounds__(256) void crc32c_long_list_kernel(SpanBatch a, Spli
       len[q] = a.len[rc];
       valid |= (r < n ? 1u : 0u) << q;
     }
-    const QuadWindow win = quad_window(off, len, valid);
+    const QuadWindow win = quad_window(a.base, off, len, valid);
     const bool lng = i < n && !((win.mask >> (i & 3u)) & 1u);
     const uint64_t m = __ballot(lng);
     if (m == 0) continue;
