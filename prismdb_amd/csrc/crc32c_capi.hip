@@ -60,7 +60,10 @@ bool g_force_generic = false;
 // Which descriptor batches go through the quad kernel first (spans of
 // <= kQuadMaxLen bytes; longer ones follow on the generic path):
 // 0 = log-record batches (PRISMDB_CRC32C_LOG_HEADER), 1 = all, -1 = none.
-int g_quad_mode = 0;
+#ifndef PRISMDB_QUAD_DEFAULT
+#define PRISMDB_QUAD_DEFAULT 0
+#endif
+int g_quad_mode = PRISMDB_QUAD_DEFAULT;
 
 void BuildTables(DeviceTables* t) {
   namespace g = prismdb::gf2;

@@ -68,6 +68,15 @@
 #ifndef PRISMDB_LOG_ROUNDSKIP  // log-record kernel: skip chunk 0's padding rounds
 #define PRISMDB_LOG_ROUNDSKIP 1
 #endif
+#ifndef PRISMDB_QUAD_NOREALIGN  // measurement knob: quad kernel skips the realignment (wrong results)
+#define PRISMDB_QUAD_NOREALIGN 0
+#endif
+#ifndef PRISMDB_QUAD_NOMASK  // measurement knob: quad kernel folds masked rounds plainly (wrong results)
+#define PRISMDB_QUAD_NOMASK 0
+#endif
+#ifndef PRISMDB_QUAD_RALIGN_GROUPS  // realignment lookups issued in this many groups (1, 2 or 4)
+#define PRISMDB_QUAD_RALIGN_GROUPS 4
+#endif
 #ifndef PRISMDB_QUAD_RING
 #define PRISMDB_QUAD_RING 2  // tasks in the quad kernel's ring (one folded, the rest in flight)
 #endif
@@ -1157,7 +1166,8 @@ __global__ __launch_bounds__(256) void crc32c_combine_kernel(SpanBatch a, SplitW
 // them that the scatter pass overwrites.
 // ---------------------------------------------------------------------------
 
-// Columns 2j and 2j+1 of shift_1, shift_2, shift_3 for the row products.
+// Columns 2j and 2j+1 of shift_1, shift_2, shift_3 (t zero bytes) for the
+// row products.
 struct RowShift {
   uint32_t c[3][2];
 };
@@ -1177,8 +1187,11 @@ __device__ __forceinline__ RowShift row_shift_cols(uint32_t j) {
   return s;
 }
 
-// shift_t(x), t = 0..3, for x and t uniform within each 16-lane row (every
-// lane of the row gets the product).
+// shift_t(x), t = 0..3, for x and t uniform within each 16-lane row: lane j
+// contributes columns 2j and 2j+1 of shift_t selected by bits 2j, 2j+1 of x,
+// and the row XOR-reduces (every lane of the row gets the product).  One
+// product, not t products of shift_1: the DPP reduction is a dependent chain,
+// and the kernel stalls on such chains, not on its instruction count.
 __device__ __forceinline__ uint32_t row_shift(const RowShift& s, uint32_t j, uint32_t x, uint32_t t) {
   // selected with masks: a ternary chain here compiles to an indexed (scratch) array
   const uint32_t m1 = t == 1u ? ~0u : 0u, m2 = t == 2u ? ~0u : 0u, m3 = t == 3u ? ~0u : 0u;
@@ -1205,6 +1218,44 @@ __device__ __forceinline__ uint32_t asm_load_dword_s(const uint8_t* sbase, uint3
   asm volatile("global_load_dword %0, %1, %2" : "=v"(r) : "v"(voff), "s"(sbase));
 #endif
   return r;
+}
+
+// Body word min(i + kAdd, wm1) of the record at sbase + bw: the index clamp,
+// the address and the load in one asm block, so hipcc cannot compute the 20
+// addresses of a task ahead of its loads (20 live VGPRs).  A VALU-written
+// VGPR read by the load right after it is interlocked (no wait states).
+template <int kAdd>
+__device__ __forceinline__ uint32_t asm_load_word_clamped(const uint8_t* sbase, uint32_t bw, uint32_t i,
+                                                          uint32_t wm1) {
+  uint32_t r, a;
+#if PRISMDB_NT_LOADS
+  asm volatile(
+      "v_add_u32 %1, %5, %2\n\t"
+      "v_min_u32 %1, %1, %3\n\t"
+      "v_lshl_add_u32 %1, %1, 2, %4\n\t"
+      "global_load_dword %0, %1, %6 nt"
+      : "=&v"(r), "=&v"(a)
+      : "v"(i), "v"(wm1), "v"(bw), "n"(kAdd), "s"(sbase));
+#else
+  asm volatile(
+      "v_add_u32 %1, %5, %2\n\t"
+      "v_min_u32 %1, %1, %3\n\t"
+      "v_lshl_add_u32 %1, %1, 2, %4\n\t"
+      "global_load_dword %0, %1, %6"
+      : "=&v"(r), "=&v"(a)
+      : "v"(i), "v"(wm1), "v"(bw), "n"(kAdd), "s"(sbase));
+#endif
+  return r;
+}
+
+template <int M, int K>
+__device__ __forceinline__ void quad_round_loads(uint32_t (&w)[kQuadRounds][4], const uint8_t* sbase, uint32_t bw,
+                                                 const uint32_t (&i0)[4], uint32_t wm1) {
+  if constexpr (M < kQuadRounds) {
+    w[M][K] = asm_load_word_clamped<64 * M>(sbase, bw, i0[K], wm1);
+    if constexpr (K == 3) quad_round_loads<M + 1, 0>(w, sbase, bw, i0, wm1);
+    else quad_round_loads<M, K + 1>(w, sbase, bw, i0, wm1);
+  }
 }
 
 __device__ __forceinline__ uint32_t asm_load_ubyte_v(uint64_t addr) {
@@ -1267,9 +1318,10 @@ struct QuadTask {
   uint32_t tb;
   const uint8_t* sbase;  // body-word loads: the window base, or `zero` when no row has body words
   const uint8_t* sb;     // the window base (edge bytes, trailers)
-  uint32_t u;  // m0 | mp << 4 | any head << 8 | any tail << 9 | any bodyless record << 10
+  uint32_t u;  // fold bounds and flags, below
 };
-constexpr uint32_t kQuadAnyH = 1u << 8, kQuadAnyT = 1u << 9, kQuadAnyW0 = 1u << 10;
+// u = m0 | mp << 4 | max h << 8 | max t << 10 | any bodyless record << 12
+constexpr uint32_t kQuadAnyW0 = 1u << 12;
 
 template <bool kVerify>
 __global__ __launch_bounds__(kThreads) void crc32c_quad_kernel(SpanBatch a) {
@@ -1306,21 +1358,18 @@ __global__ __launch_bounds__(kThreads) void crc32c_quad_kernel(SpanBatch a) {
   // Issue task tb: descriptors (scalar), the lane's row geometry (vector),
   // the fold bounds (four readlanes), 21 loads.
   // vmeta = W | P << 9 | h << 18 | t << 20 | ok << 22 | edge-byte-used << 23;
-  // vr0 = init ^ ~0; vpo = offset of the record's first byte from sbase.
+  // vpo = offset of the record's first byte from sbase.  (The init values
+  // are read at fold time: one VGPR less per ring slot.)
   auto issue = [&](uint32_t tb, uint32_t (&w)[kQuadRounds][4], uint32_t& e, QuadTask& tk, uint32_t& vmeta,
-                   uint32_t& vr0, uint32_t& vpo) {
+                   uint32_t& vpo) {
     uint64_t off[4];
-    uint32_t len[4], ini[4] = {0u, 0u, 0u, 0u}, valid;
+    uint32_t len[4], valid;
     if (tb + 4u <= n) {  // one contiguous scalar read per array
       valid = 15u;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         off[q] = const_load(a.off + tb, (uint64_t)q);
         len[q] = const_load(a.len + tb, (uint64_t)q);
-      }
-      if (a.init != nullptr) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) ini[q] = const_load(a.init + tb, (uint64_t)q);
       }
     } else {  // the batch's last task (or past it): clamped reads
       const uint32_t last = n - 1u;
@@ -1330,7 +1379,6 @@ __global__ __launch_bounds__(kThreads) void crc32c_quad_kernel(SpanBatch a) {
         const uint32_t i = tb + (uint32_t)q < last ? tb + (uint32_t)q : last;
         off[q] = const_load(a.off, i);
         len[q] = const_load(a.len, i);
-        if (a.init != nullptr) ini[q] = const_load(a.init, i);
         valid |= (tb + (uint32_t)q < n ? 1u : 0u) << q;
       }
     }
@@ -1342,7 +1390,6 @@ __global__ __launch_bounds__(kThreads) void crc32c_quad_kernel(SpanBatch a) {
     const uint32_t ln = sel(len[0], len[1], len[2], len[3]);
     const bool ok = (win.mask >> g) & 1u;
     vpo = ok ? base_sb + sel((uint32_t)off[0], (uint32_t)off[1], (uint32_t)off[2], (uint32_t)off[3]) : 8u;
-    vr0 = sel(ini[0], ini[1], ini[2], ini[3]) ^ kConditioning;
     // head bytes up to 4-B alignment of the absolute address
     uint32_t h = (0u - ((uint32_t)win.sb + vpo)) & 3u;
     h = h < ln ? h : ln;
@@ -1353,12 +1400,14 @@ __global__ __launch_bounds__(kThreads) void crc32c_quad_kernel(SpanBatch a) {
     // fold bounds: rounds from 5 - Rmax, masked through mp (rows without
     // body words read someone else's bytes: all rounds masked); flags
     const uint32_t R = (W + 63u) >> 6, mpv = W ? P >> 6 : (uint32_t)kQuadRounds;
-    const uint32_t pk = R | (mpv << 4) | (h ? kQuadAnyH : 0u) | (t ? kQuadAnyT : 0u) |
-                        (ok && W == 0u ? kQuadAnyW0 : 0u);
+    const uint32_t pk = R | (mpv << 4) | (h << 8) | (t << 10) | (ok && W == 0u ? kQuadAnyW0 : 0u);
     const uint32_t p0 = readlane(pk, 0), p1 = readlane(pk, 16), p2 = readlane(pk, 32), p3 = readlane(pk, 48);
-    const uint32_t rmax = max(max(p0 & 15u, p1 & 15u), max(p2 & 15u, p3 & 15u));
-    const uint32_t mp = max(max((p0 >> 4) & 15u, (p1 >> 4) & 15u), max((p2 >> 4) & 15u, (p3 >> 4) & 15u));
-    tk.u = ((uint32_t)kQuadRounds - rmax) | (mp << 4) | ((p0 | p1 | p2 | p3) & (kQuadAnyH | kQuadAnyT | kQuadAnyW0));
+    auto fmax = [&](int sh, uint32_t m) {
+      return max(max((p0 >> sh) & m, (p1 >> sh) & m), max((p2 >> sh) & m, (p3 >> sh) & m));
+    };
+    const uint32_t rmax = fmax(0, 15u), mp = fmax(4, 15u);
+    tk.u = ((uint32_t)kQuadRounds - rmax) | (mp << 4) | (fmax(8, 3u) << 8) | (fmax(10, 3u) << 10) |
+           ((p0 | p1 | p2 | p3) & kQuadAnyW0);
     // Body words: frame position 64 m + v is body word 64 m + v - P, clamped
     // into the record (the fold zeroes the words outside it).  A row without
     // body words reads the first body word of the first row that has some
@@ -1378,14 +1427,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_quad_kernel(SpanBatch a) {
       i0[k] = vlane(k) - P;
       asm volatile("" : "+v"(i0[k]));
     }
-#pragma unroll
-    for (int m = 0; m < kQuadRounds; ++m) {
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const uint32_t idx = i0[k] + 64u * (uint32_t)m;
-        w[m][k] = asm_load_dword_s(tk.sbase, bw + 4u * (idx < wm1 ? idx : wm1));
-      }
-    }
+    quad_round_loads<0, 0>(w, tk.sbase, bw, i0, wm1);
     // Edge byte: quad 0 of the row loads head byte o (o < h), quad 1 tail
     // byte o (o < t), quad 2 stored-crc byte o (verify); the rest are masked.
     const uint32_t qd = j >> 2, o = j & 3u;
@@ -1408,7 +1450,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_quad_kernel(SpanBatch a) {
 
   uint32_t res = 0u, bad = 0u;
   auto fold = [&](const QuadTask& tk, const uint32_t (&w)[kQuadRounds][4], uint32_t e, uint32_t vmeta,
-                  uint32_t vr0, uint32_t vpo) {
+                  uint32_t vpo) {
     const uint32_t W = vmeta & 511u, P = (vmeta >> 9) & 511u, h = (vmeta >> 18) & 3u, t = (vmeta >> 20) & 3u;
     const bool ok = (vmeta >> 22) & 1u;
     const uint32_t m0 = tk.u & 15u, mp = (tk.u >> 4) & 15u;
@@ -1416,8 +1458,15 @@ __global__ __launch_bounds__(kThreads) void crc32c_quad_kernel(SpanBatch a) {
     // (head), quad 1 (tail), quad 2 (stored crc).
     uint32_t ew = ((vmeta >> 23) & 1u) ? e << (8u * (j & 3u)) : 0u;
     ew = xor_dpp(xor_dpp(ew, 0xB1), 0x4E);
-    uint32_t r = vr0;  // register before the head bytes
-    if (tk.u & kQuadAnyH) r = row_shift(rsh, j, r ^ row_bcast<0>(ew), h);
+    uint32_t r = kConditioning;  // register before the head bytes: init ^ ~0
+    if (a.init != nullptr) {
+      uint32_t iv[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) iv[q] = const_load(a.init, tk.tb + (uint32_t)q < n ? tk.tb + (uint32_t)q : n - 1u);
+      r ^= sel(iv[0], iv[1], iv[2], iv[3]);
+    }
+    const uint32_t hmax = (tk.u >> 8) & 3u, tmax = (tk.u >> 10) & 3u;
+    if (hmax) r = row_shift(rsh, j, r ^ row_bcast<0>(ew), h);
     uint32_t acc[4] = {0u, 0u, 0u, 0u};
     uint32_t i0[4];  // as in issue(): opaque per-task indices
 #pragma unroll
@@ -1428,7 +1477,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_quad_kernel(SpanBatch a) {
 #pragma unroll
     for (int m = 0; m < kQuadRounds; ++m) {
       if ((uint32_t)m < m0) continue;
-      if ((uint32_t)m <= mp) {
+      if (!PRISMDB_QUAD_NOMASK && (uint32_t)m <= mp) {
         // positions before the body read 0, body word 0 carries the register
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -1444,15 +1493,19 @@ __global__ __launch_bounds__(kThreads) void crc32c_quad_kernel(SpanBatch a) {
     }
     // one sub-stream's eight lookups at a time (the memory clobber keeps the
     // next batch of LDS reads below): 32 in flight at once cost 24 spilled VGPRs
+#if PRISMDB_QUAD_NOREALIGN
+    uint32_t x = xor3(acc[0], acc[1], acc[2]) ^ acc[3];
+#else
     uint32_t x = realign(lds, nib[0], acc[0]);
 #pragma unroll
     for (int k = 1; k < 4; ++k) {
-      asm volatile("" ::: "memory");
+      if (k % (4 / PRISMDB_QUAD_RALIGN_GROUPS) == 0) asm volatile("" ::: "memory");
       x ^= realign(lds, nib[k], acc[k]);
     }
+#endif
     x = row_xor(x);
     if (tk.u & kQuadAnyW0) x = W == 0u ? r : x;  // no body words: the register after the head
-    if (tk.u & kQuadAnyT) x = row_shift(rsh, j, x ^ row_bcast<4>(ew), t);
+    if (tmax) x = row_shift(rsh, j, x ^ row_bcast<4>(ew), t);
     const uint32_t crc = x ^ kConditioning;
     const uint32_t v = (a.flags & kFlagMask) ? mask_crc(crc) : crc;
     if ((a.flags & kFlagWriteTrailer) && ok && j == 0u)
@@ -1471,10 +1524,13 @@ __global__ __launch_bounds__(kThreads) void crc32c_quad_kernel(SpanBatch a) {
     // Run end: one coalesced store of the run's results (placeholders for
     // listed spans, rewritten by the scatter pass).
     if (tir == 15u || tk.tb + 4u >= n) {
-      const uint32_t rb = tk.tb & ~63u;
-      if (rb + lane < n) {
-        if (a.out != nullptr) __builtin_nontemporal_store(res, a.out + rb + lane);
-        if (kVerify && a.mismatch != nullptr) __builtin_nontemporal_store((uint8_t)bad, a.mismatch + rb + lane);
+      // the record index is opaque so hipcc does not keep a.out + lane and
+      // a.mismatch + lane live across the loop (64-bit pointers per lane)
+      uint32_t rec = (tk.tb & ~63u) + lane;
+      asm volatile("" : "+v"(rec));
+      if (rec < n) {
+        if (a.out != nullptr) __builtin_nontemporal_store(res, a.out + rec);
+        if (kVerify && a.mismatch != nullptr) __builtin_nontemporal_store((uint8_t)bad, a.mismatch + rec);
       }
     }
   };
@@ -1486,20 +1542,20 @@ __global__ __launch_bounds__(kThreads) void crc32c_quad_kernel(SpanBatch a) {
   uint32_t wq[kRing][kQuadRounds][4];
   uint32_t eq[kRing];
   QuadTask tq[kRing];
-  uint32_t vm[kRing], vr[kRing], vp[kRing];
+  uint32_t vm[kRing], vp[kRing];
   uint32_t ahead = cur;
 #pragma unroll
   for (int d = 0; d < kRing; ++d) {
-    issue(ahead, wq[d], eq[d], tq[d], vm[d], vr[d], vp[d]);
+    issue(ahead, wq[d], eq[d], tq[d], vm[d], vp[d]);
     ahead = adv(ahead);
   }
   for (;;) {
 #pragma unroll
     for (int sl = 0; sl < kRing; ++sl) {
       wait_quad<kYounger>(wq[sl], eq[sl]);
-      if (tq[sl].tb < n) fold(tq[sl], wq[sl], eq[sl], vm[sl], vr[sl], vp[sl]);
+      if (tq[sl].tb < n) fold(tq[sl], wq[sl], eq[sl], vm[sl], vp[sl]);
       cur = adv(cur);
-      issue(ahead, wq[sl], eq[sl], tq[sl], vm[sl], vr[sl], vp[sl]);
+      issue(ahead, wq[sl], eq[sl], tq[sl], vm[sl], vp[sl]);
       ahead = adv(ahead);
     }
     if (cur >= n) break;

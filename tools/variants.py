@@ -38,6 +38,17 @@ VARIANTS = {
     "snop": {"PRISMDB_SPAN_SNOP": 1},
     # fixed kernel: runs of 16 spans per wave instead of 64
     "run3": {"PRISMDB_RUN_LG": 3},
+    # quad kernel (short records): measurement-only cuts (wrong results) and
+    # the realignment lookups in 2 groups / 1 group instead of 4
+    "quad_norealign": {"PRISMDB_QUAD_NOREALIGN": 1},
+    "quad_nomask": {"PRISMDB_QUAD_NOMASK": 1},
+    "quad_ra2": {"PRISMDB_QUAD_RALIGN_GROUPS": 2},
+    "quad_ra1": {"PRISMDB_QUAD_RALIGN_GROUPS": 1},
+    # every descriptor batch through the quad kernel first
+    "quad_all": {"PRISMDB_QUAD_DEFAULT": 1},
+    # quad kernel ring depth (tasks in flight + 1)
+    "quad_r2": {"PRISMDB_QUAD_RING": 2},
+    "quad_r3": {"PRISMDB_QUAD_RING": 3},
 }
 # Measured and dropped (profiles/r01_variants_ring_runs.json): refilling a ring
 # pair before its fold with a 6-buffer ring ("early6") was no faster.
