@@ -195,7 +195,7 @@ struct Workspace {
   void* mem = nullptr;
   char* grow = nullptr;
   size_t cap_rec = 0;
-  char* qgrow = nullptr;  // quad path: long-span list and its results, 9 B per span
+  char* qgrow = nullptr;  // quad path: long-span list and its results (9 B per span), run flags
   size_t cap_q = 0;
   SplitWs ws{};
 };
@@ -259,13 +259,14 @@ int GetWorkspace(hipStream_t s, size_t nspans, uint32_t streams, bool quad, Spli
       w.cap_q = 0;
     }
     const size_t cap = nspans < 4096 ? 4096 : nspans + nspans / 4;
-    hipError_t e = hipMalloc(reinterpret_cast<void**>(&w.qgrow), cap * 9 + 16);
+    hipError_t e = hipMalloc(reinterpret_cast<void**>(&w.qgrow), cap * 9 + cap / 64 + 1024);
     if (e != hipSuccess) return FailHip(e, "quad list workspace hipMalloc");
     w.cap_q = cap;
   }
   w.ws.list = quad ? reinterpret_cast<uint32_t*>(w.qgrow) : nullptr;
   w.ws.qout = quad ? reinterpret_cast<uint32_t*>(w.qgrow + w.cap_q * 4) : nullptr;
   w.ws.qmm = quad ? reinterpret_cast<uint8_t*>(w.qgrow + w.cap_q * 8) : nullptr;
+  w.ws.qrun = quad ? reinterpret_cast<uint8_t*>(w.qgrow + w.cap_q * 9) : nullptr;
   w.ws.rec = reinterpret_cast<prismdb::dev::SpanRec*>(w.grow);
   w.ws.slice_start = reinterpret_cast<uint64_t*>(w.grow + w.cap_rec * 16);
   w.ws.cnt = reinterpret_cast<uint32_t*>(w.grow + w.cap_rec * 16 + SliceCap(w.cap_rec, streams) * 8);
@@ -329,6 +330,7 @@ int RunBatch(DeviceCtx& ctx, const SpanBatch& base_args, bool desc, bool verify,
   uint32_t* const caller_out = a.out;
   uint8_t* const caller_mm = a.mismatch;
   if (quad) {
+    a.qrun = ws.qrun;
     e = prismdb::dev::launch_quad(a, verify, ctx.cus, ws, s);
     if (e != hipSuccess) return FailHip(e, "quad kernel launch");
     a.idx = ws.list;

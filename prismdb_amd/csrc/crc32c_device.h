@@ -37,6 +37,8 @@ constexpr int kLdsWords = kTabWords + kNibWords;   // 160 KiB: all of a CU's LDS
 constexpr uint32_t kLongSpan = 128u * 1024u;       // spans above this are split...
 constexpr uint32_t kSegment = 32u * 1024u;         // ...into pieces of this size
 
+constexpr int kZeroWords = 16384;  // DeviceTables::zero: 256 regions of 256 B
+
 // Tables derived on the host from the polynomial (crc32c_gf2.h) and kept in HBM.
 struct DeviceTables {
   uint32_t stride[4][256];    // stride[k][b] = shift_256(b << 8k)
@@ -44,7 +46,10 @@ struct DeviceTables {
   uint32_t shift_seg[32];     // column i of shift_kSegment (M)
   uint32_t shift_seg64[32];   // column i of M^64
   uint32_t lane_seg[32][64];  // [i][l] = column i of M^(63-l): lane l's final shift
-  uint32_t zero[4];           // 16 zero bytes: the quad kernel's loads of unused lanes land here
+  // 64 KiB of zeros: the quad kernel's loads of lanes without a record to
+  // read land here, 256 B per wave (wave % 256) -- one shared line was an L2
+  // hotspot when whole tasks are left to the generic path
+  uint32_t zero[kZeroWords];
 };
 
 // Short-record ("quad") kernel: spans of len <= kQuadMaxLen, four per wave,
@@ -87,6 +92,7 @@ struct SpanBatch {
   // descriptors and results (the generic path behind the quad kernel runs
   // over the list of spans too long for it; n_dev holds the list length)
   const uint32_t* idx;
+  const uint8_t* qrun;  // quad kernel: runs it owns a span of (crc32c_long_list_kernel)
 };
 
 struct SplitCounters {
@@ -119,6 +125,7 @@ struct SplitWs {
   uint32_t* list;         // quad path: indices of the spans longer than kQuadMaxLen
   uint32_t* qout;         // quad path: generic-path results of the listed spans (list order)
   uint8_t* qmm;
+  uint8_t* qrun;          // quad path: per run of 64 spans, 1 if the quad kernel owns one of them
 };
 
 constexpr uint32_t kMaxPlanBlocks = 4096;
@@ -132,6 +139,7 @@ hipError_t launch_slices(const SpanBatch& a, const SplitWs& ws, hipStream_t s);
 hipError_t launch_combine(const SpanBatch& a, bool desc, bool verify, const SplitWs& ws,
                           hipStream_t s);
 hipError_t launch_quad(const SpanBatch& a, bool verify, int grid, const SplitWs& ws, hipStream_t s);
+constexpr int kListThreads = 1024;  // crc32c_long_list_kernel block: one atomic per 16 runs
 hipError_t launch_scatter(const SpanBatch& a, const SplitWs& ws, const uint32_t* qout, const uint8_t* qmm,
                           hipStream_t s);
 

@@ -1322,6 +1322,7 @@ struct QuadTask {
 };
 // u = m0 | mp << 4 | max h << 8 | max t << 10 | any bodyless record << 12
 constexpr uint32_t kQuadAnyW0 = 1u << 12;
+constexpr uint32_t kQuadOwned = 1u << 13;  // the kernel owns at least one of the task's records
 
 template <bool kVerify>
 __global__ __launch_bounds__(kThreads) void crc32c_quad_kernel(SpanBatch a) {
@@ -1343,12 +1344,20 @@ __global__ __launch_bounds__(kThreads) void crc32c_quad_kernel(SpanBatch a) {
   const uint32_t nwaves = gridDim.x * kWavesPerGroup;
   // Runs of 64 records (16 tasks), run r of wave w = records [(r nwaves + w) 64, +64).
   // (tb < n + 64 nwaves always, far below 2^32.)
-  const uint32_t jump = (nwaves - 1u) * 64u + 4u;
-  auto adv = [&](uint32_t tb) -> uint32_t { return ((tb + 4u) & 63u) ? tb + 4u : tb + jump; };
-  uint32_t cur = wave * 64u;
+  // Runs the quad kernel owns nothing of (ws-side flags from the list
+  // kernel, read through the scalar cache) are skipped whole.
+  const uint8_t* const qrun = a.qrun;
+  auto next_run = [&](uint32_t rb) -> uint32_t {  // first owned run at or after rb, its first record
+    while (rb < n && const_load(qrun, (uint64_t)(rb >> 6)) == 0u) rb += 64u * nwaves;
+    return rb;
+  };
+  auto adv = [&](uint32_t tb) -> uint32_t {
+    return ((tb + 4u) & 63u) ? tb + 4u : next_run((tb & ~63u) + 64u * nwaves);
+  };
+  uint32_t cur = next_run(wave * 64u);
   if (cur >= n) return;
   const bool hdr = (a.flags & kFlagLogHeader) != 0;
-  const uint8_t* const zero = reinterpret_cast<const uint8_t*>(&a.tabs->zero[0]);
+  const uint8_t* const zero = reinterpret_cast<const uint8_t*>(&a.tabs->zero[0]) + 256u * (wave & 255u);
 
   // The lane's row's value out of four uniform ones.
   auto sel = [&](uint32_t x0, uint32_t x1, uint32_t x2, uint32_t x3) -> uint32_t {
@@ -1407,7 +1416,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_quad_kernel(SpanBatch a) {
     };
     const uint32_t rmax = fmax(0, 15u), mp = fmax(4, 15u);
     tk.u = ((uint32_t)kQuadRounds - rmax) | (mp << 4) | (fmax(8, 3u) << 8) | (fmax(10, 3u) << 10) |
-           ((p0 | p1 | p2 | p3) & kQuadAnyW0);
+           ((p0 | p1 | p2 | p3) & kQuadAnyW0) | (win.mask ? kQuadOwned : 0u);
     // Body words: frame position 64 m + v is body word 64 m + v - P, clamped
     // into the record (the fold zeroes the words outside it).  A row without
     // body words reads the first body word of the first row that has some
@@ -1493,17 +1502,22 @@ __global__ __launch_bounds__(kThreads) void crc32c_quad_kernel(SpanBatch a) {
     }
     // one sub-stream's eight lookups at a time (the memory clobber keeps the
     // next batch of LDS reads below): 32 in flight at once cost 24 spilled VGPRs
+    // A task of records all left to the generic path folds no round (its
+    // rows have no body words) and skips the realignment as well.
+    uint32_t x = 0u;
+    if (tk.u & kQuadOwned) {
 #if PRISMDB_QUAD_NOREALIGN
-    uint32_t x = xor3(acc[0], acc[1], acc[2]) ^ acc[3];
+      x = xor3(acc[0], acc[1], acc[2]) ^ acc[3];
 #else
-    uint32_t x = realign(lds, nib[0], acc[0]);
+      x = realign(lds, nib[0], acc[0]);
 #pragma unroll
-    for (int k = 1; k < 4; ++k) {
-      if (k % (4 / PRISMDB_QUAD_RALIGN_GROUPS) == 0) asm volatile("" ::: "memory");
-      x ^= realign(lds, nib[k], acc[k]);
-    }
+      for (int k = 1; k < 4; ++k) {
+        if (k % (4 / PRISMDB_QUAD_RALIGN_GROUPS) == 0) asm volatile("" ::: "memory");
+        x ^= realign(lds, nib[k], acc[k]);
+      }
 #endif
-    x = row_xor(x);
+      x = row_xor(x);
+    }
     if (tk.u & kQuadAnyW0) x = W == 0u ? r : x;  // no body words: the register after the head
     if (tmax) x = row_shift(rsh, j, x ^ row_bcast<4>(ew), t);
     const uint32_t crc = x ^ kConditioning;
@@ -1574,14 +1588,20 @@ __global__ __launch_bounds__(kThreads) void crc32c_quad_kernel(SpanBatch a) {
 }
 
 // The spans the quad kernel leaves to the generic path (len > kQuadMaxLen, or
-// outside their task's window), listed in runs of one wave's 64 consecutive
-// spans; ws.counters->nlist is the count.
-__global__ __launch_bounds__(256) void crc32c_long_list_kernel(SpanBatch a, SplitWs ws) {
+// outside their task's window), listed run by run (a wave's 64 consecutive
+// spans stay together and in order); ws.counters->nlist is the count.  One
+// atomic per block of 16 runs (one per run serialized on the counter: 790 us
+// for 64 Ki runs).  ws.qrun[r] = 1 if the quad kernel owns a span of run r:
+// it skips the other runs.
+__global__ __launch_bounds__(kListThreads) void crc32c_long_list_kernel(SpanBatch a, SplitWs ws) {
   const uint64_t n = a.n;
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint64_t step = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); b < n; b += step) {
-    const uint64_t i = b + lane;
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  constexpr uint32_t kWaves = kListThreads / 64;
+  __shared__ uint32_t cnt[kWaves];
+  __shared__ unsigned long long base;
+  const uint64_t step = (uint64_t)gridDim.x * kListThreads;
+  for (uint64_t b0 = (uint64_t)blockIdx.x * kListThreads; b0 < n; b0 += step) {
+    const uint64_t i = b0 + 64u * wv + lane;
     // the task (4-aligned quad of records) this lane's record belongs to
     const uint64_t t0 = i & ~3ull;
     uint64_t off[4];
@@ -1595,13 +1615,25 @@ __global__ __launch_bounds__(256) void crc32c_long_list_kernel(SpanBatch a, Spli
       valid |= (r < n ? 1u : 0u) << q;
     }
     const QuadWindow win = quad_window(a.base, off, len, valid);
-    const bool lng = i < n && !((win.mask >> (i & 3u)) & 1u);
+    const bool mine = i < n && ((win.mask >> (i & 3u)) & 1u);
+    const bool lng = i < n && !mine;
     const uint64_t m = __ballot(lng);
-    if (m == 0) continue;
-    unsigned long long pos = 0;
-    if (lane == 0) pos = atomicAdd(&ws.counters->nlist, (unsigned long long)__popcll(m));
-    pos = __shfl(pos, 0);
+    const uint64_t own = __ballot(mine);
+    if (lane == 0) {
+      cnt[wv] = (uint32_t)__popcll(m);
+      if (i < n) ws.qrun[i >> 6] = own ? 1u : 0u;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint32_t tot = 0;
+      for (uint32_t k = 0; k < kWaves; ++k) tot += cnt[k];
+      base = tot ? atomicAdd(&ws.counters->nlist, (unsigned long long)tot) : 0ull;
+    }
+    __syncthreads();
+    uint64_t pos = base;
+    for (uint32_t k = 0; k < wv; ++k) pos += cnt[k];
     if (lng) ws.list[pos + (uint64_t)__popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)i;
+    __syncthreads();  // cnt/base are rewritten by the next iteration
   }
 }
 
@@ -1666,8 +1698,8 @@ hipError_t launch_slices(const SpanBatch& a, const SplitWs& ws, hipStream_t s) {
 }
 
 hipError_t launch_quad(const SpanBatch& a, bool verify, int grid, const SplitWs& ws, hipStream_t s) {
-  const int lgrid = (int)((a.n + 255u) / 256u < 2048u ? (a.n + 255u) / 256u : 2048u);
-  crc32c_long_list_kernel<<<lgrid, 256, 0, s>>>(a, ws);
+  const uint64_t lb = (a.n + kListThreads - 1) / kListThreads;
+  crc32c_long_list_kernel<<<(int)(lb < 1024u ? lb : 1024u), kListThreads, 0, s>>>(a, ws);
   if (verify) crc32c_quad_kernel<true><<<grid, kThreads, 0, s>>>(a);
   else crc32c_quad_kernel<false><<<grid, kThreads, 0, s>>>(a);
   return hipGetLastError();
