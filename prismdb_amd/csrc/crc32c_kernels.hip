@@ -1369,29 +1369,40 @@ __global__ __launch_bounds__(kThreads) void crc32c_quad_kernel(SpanBatch a) {
   // vmeta = W | P << 9 | h << 18 | t << 20 | ok << 22 | edge-byte-used << 23;
   // vpo = offset of the record's first byte from sbase.  (The init values
   // are read at fold time: one VGPR less per ring slot.)
-  auto issue = [&](uint32_t tb, uint32_t (&w)[kQuadRounds][4], uint32_t& e, QuadTask& tk, uint32_t& vmeta,
-                   uint32_t& vpo) {
+  // A task's four descriptors, read through the scalar cache one task ahead
+  // (before the wait for the slot being folded, so the read's latency hides
+  // behind that wait instead of stalling issue()).
+  struct QuadDesc {
     uint64_t off[4];
     uint32_t len[4], valid;
+  };
+  auto fetch = [&](uint32_t tb) -> QuadDesc {
+    QuadDesc d;
     if (tb + 4u <= n) {  // one contiguous scalar read per array
-      valid = 15u;
+      d.valid = 15u;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        off[q] = const_load(a.off + tb, (uint64_t)q);
-        len[q] = const_load(a.len + tb, (uint64_t)q);
+        d.off[q] = const_load(a.off + tb, (uint64_t)q);
+        d.len[q] = const_load(a.len + tb, (uint64_t)q);
       }
     } else {  // the batch's last task (or past it): clamped reads
       const uint32_t last = n - 1u;
-      valid = 0u;
+      d.valid = 0u;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const uint32_t i = tb + (uint32_t)q < last ? tb + (uint32_t)q : last;
-        off[q] = const_load(a.off, i);
-        len[q] = const_load(a.len, i);
-        valid |= (tb + (uint32_t)q < n ? 1u : 0u) << q;
+        d.off[q] = const_load(a.off, i);
+        d.len[q] = const_load(a.len, i);
+        d.valid |= (tb + (uint32_t)q < n ? 1u : 0u) << q;
       }
     }
-    const QuadWindow win = quad_window(a.base, off, len, valid);
+    return d;
+  };
+  auto issue = [&](uint32_t tb, const QuadDesc& d, uint32_t (&w)[kQuadRounds][4], uint32_t& e, QuadTask& tk,
+                   uint32_t& vmeta, uint32_t& vpo) {
+    const uint64_t(&off)[4] = d.off;
+    const uint32_t(&len)[4] = d.len;
+    const QuadWindow win = quad_window(a.base, off, len, d.valid);
     tk.tb = tb;
     tk.sb = reinterpret_cast<const uint8_t*>(win.sb);
     // the row's record in 32 bits: its offset from sbase fits 31 bits
@@ -1560,16 +1571,17 @@ __global__ __launch_bounds__(kThreads) void crc32c_quad_kernel(SpanBatch a) {
   uint32_t ahead = cur;
 #pragma unroll
   for (int d = 0; d < kRing; ++d) {
-    issue(ahead, wq[d], eq[d], tq[d], vm[d], vp[d]);
+    issue(ahead, fetch(ahead), wq[d], eq[d], tq[d], vm[d], vp[d]);
     ahead = adv(ahead);
   }
   for (;;) {
 #pragma unroll
     for (int sl = 0; sl < kRing; ++sl) {
+      const QuadDesc nd = fetch(ahead);  // ahead of the wait (its memory clobber keeps it there)
       wait_quad<kYounger>(wq[sl], eq[sl]);
       if (tq[sl].tb < n) fold(tq[sl], wq[sl], eq[sl], vm[sl], vp[sl]);
       cur = adv(cur);
-      issue(ahead, wq[sl], eq[sl], tq[sl], vm[sl], vp[sl]);
+      issue(ahead, nd, wq[sl], eq[sl], tq[sl], vm[sl], vp[sl]);
       ahead = adv(ahead);
     }
     if (cur >= n) break;

@@ -1,0 +1,15 @@
+#!/bin/bash
+# A/B: quad kernel with descriptors fetched one task ahead (pref) vs before (base); GPU suite + smoke
+set -o pipefail
+O=gpurun_out; mkdir -p $O
+timeout -k 10 600 python tools/variants.py run --only base pref --gib 16 --reps 10 > $O/r02o_variants.json 2> $O/r02o_variants.err || exit $?
+python - <<'PY'
+import json
+d = json.load(open("gpurun_out/r02o_variants.json"))
+print({k: v for k, v in d["agree"].items() if not v})
+for w, r in d["results"].items():
+    print(w, {n: v["GB/s_median"] for n, v in r.items()})
+PY
+timeout -k 10 900 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 300 --timeout-method thread -x > $O/r02o_tests.log 2>&1
+rc=$?; tail -2 $O/r02o_tests.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" 2>&1 | tail -1
