@@ -203,7 +203,12 @@ struct Workspace {
 // Slice starts needed for n spans: nslices + 1 <= n/2 + 32 * streams + 2
 // (crc32c_slice_scan_kernel: tau = 64 gives <= n/2 + 1 slices of <= 32-task
 // spans; a smaller tau keeps tau > T / (32 * streams)).
-size_t SliceCap(size_t n, uint32_t streams) { return n / 2 + 32 * (size_t)streams + 4; }
+#ifndef PRISMDB_SLICES_PER_STREAM
+#define PRISMDB_SLICES_PER_STREAM 16
+#endif
+size_t SliceCap(size_t n, uint32_t streams) {
+  return n / 2 + 2 * (size_t)PRISMDB_SLICES_PER_STREAM * streams + 4;
+}
 
 constexpr uint64_t kCapSeg = 1u << 20;   // 1 Mi segments = 32 GiB of long spans per call
 constexpr uint32_t kCapLong = 1u << 18;

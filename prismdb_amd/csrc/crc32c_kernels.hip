@@ -77,6 +77,12 @@
 #ifndef PRISMDB_QUAD_RALIGN_GROUPS  // realignment lookups issued in this many groups (1, 2 or 4)
 #define PRISMDB_QUAD_RALIGN_GROUPS 4
 #endif
+#ifndef PRISMDB_SLICES_PER_STREAM  // span kernel: task-balanced slices shrink until every stream gets this many
+#define PRISMDB_SLICES_PER_STREAM 16
+#endif
+#ifndef PRISMDB_RUNS_PER_STREAM  // span kernel: runs of one-task records shrink until every stream gets this many
+#define PRISMDB_RUNS_PER_STREAM 64
+#endif
 #ifndef PRISMDB_QUAD_RING
 #define PRISMDB_QUAD_RING 2  // tasks in the quad kernel's ring (one folded, the rest in flight)
 #endif
@@ -475,7 +481,11 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
   // together (dealt equal record counts, config 3's busiest stream had 26 %
   // more tasks than the mean, and a wave folds its two streams in lockstep).  Segment role: slices of kRun records (segments are all but
   // uniform; so are span-role batches whose spans are one task each), kRun =
-  // 64 shortened so every stream gets >= 16 slices.  A slice
+  // 64 shortened so every stream gets >= PRISMDB_RUNS_PER_STREAM (64) of them:
+  // a stream's count is ceil or floor of the mean, and with 16 runs per
+  // stream the rounding left SST-shaped batches up to 3.6 % in the tail
+  // (profiles/r02p_variants_slices_runs.json; the task-balanced slices keep
+  // >= 16: smaller slices cost the config-3 mix 9 %).  A slice
   // holds at most 64 records: lane i of res[s] / bad[s] collects its i-th
   // result / verify flag, stored with one coalesced nt store when the slice's
   // last record retires (scattered 4-byte stores cost 10 % of the read rate;
@@ -486,7 +496,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
   uint32_t K = sliced ? (uint32_t)const_load(a.nslices_dev, 0) : 0u;  // <= n/2 + 32 S + 2; 0: runs
   if (K == 0) {
     sliced = false;
-    while (lg > 0 && (n >> (lg + 1)) < nwaves * 16u) --lg;
+    while (lg > 0 && (n >> (lg + 1)) < nwaves * (uint32_t)PRISMDB_RUNS_PER_STREAM) --lg;
     K = (uint32_t)(((uint64_t)n + (1u << lg) - 1) >> lg);
   }
   // Per stream: the pending record b (the one after the stream's newest task)
@@ -1040,7 +1050,7 @@ __global__ __launch_bounds__(1024) void crc32c_slice_scan_kernel(SpanBatch a, Sp
   if (t == 0) {
     const uint64_t S = ws.nstreams;
     uint32_t lg = 6;
-    while (lg > 0 && (T >> lg) < S * 16u) --lg;
+    while (lg > 0 && (T >> lg) < S * (uint64_t)PRISMDB_SLICES_PER_STREAM) --lg;
     const uint64_t K = (T + (1ull << lg) - 1) >> lg;
     ws.counters->tasks = T;
     ws.counters->lg_tau = lg;

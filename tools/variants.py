@@ -46,6 +46,12 @@ VARIANTS = {
     "quad_ra1": {"PRISMDB_QUAD_RALIGN_GROUPS": 1},
     # every descriptor batch through the quad kernel first
     "quad_all": {"PRISMDB_QUAD_DEFAULT": 1},
+    # span kernel: at least 64 / 256 slices per record stream (finer tail balance)
+    "slices64": {"PRISMDB_SLICES_PER_STREAM": 64},
+    "slices256": {"PRISMDB_SLICES_PER_STREAM": 256},
+    # span kernel runs mode (one-task records): 16 runs per stream (round 1) / 256
+    "runs16": {"PRISMDB_RUNS_PER_STREAM": 16},
+    "runs256": {"PRISMDB_RUNS_PER_STREAM": 256},
     # quad kernel ring depth (tasks in flight + 1)
     "quad_r2": {"PRISMDB_QUAD_RING": 2},
     "quad_r3": {"PRISMDB_QUAD_RING": 3},
