@@ -80,6 +80,9 @@
 #ifndef PRISMDB_SLICES_PER_STREAM  // span kernel: task-balanced slices shrink until every stream gets this many
 #define PRISMDB_SLICES_PER_STREAM 16
 #endif
+#ifndef PRISMDB_SLICE_EXACT  // task-balanced slices: exactly m per stream (1) or ceil(T / 2^lg) (0)
+#define PRISMDB_SLICE_EXACT 1
+#endif
 #ifndef PRISMDB_RUNS_PER_STREAM  // span kernel: runs of one-task records shrink until every stream gets this many
 #define PRISMDB_RUNS_PER_STREAM 64
 #endif
@@ -1049,11 +1052,30 @@ __global__ __launch_bounds__(1024) void crc32c_slice_scan_kernel(SpanBatch a, Sp
   }
   if (t == 0) {
     const uint64_t S = ws.nstreams;
+#if PRISMDB_SLICE_EXACT
+    // K = m S slices, so every stream gets exactly m of them (dealt s, s+S,
+    // ...): with K = ceil(T / 2^lg) a stream got ceil or floor of K/S and the
+    // ceil streams set the kernel's end (config 3: 17 slices against a mean of
+    // 16.6).  Slice k = tasks [k q + min(k, r), ...) with q = T / K, r = T % K.
+    // At most 64 tasks per slice (q <= 63), so at most 64 records (a lane
+    // per result); at least 16 slices per stream while they stay >= 32 tasks
+    // (a slice of >= 32 tasks always starts a record: spans are <= 32 tasks).
+    const uint64_t per = (uint64_t)PRISMDB_SLICES_PER_STREAM;
+    uint64_t m = (T + 63u * S - 1u) / (63u * S);
+    const uint64_t m32 = T / (32u * S);
+    if (m < per && m32 > m) m = m32 < per ? m32 : per;
+    if (m < 1u) m = 1u;
+    uint64_t K = m * S;
+    if (K > T) K = T > 0 ? T : 1u;
+    ws.counters->slice_q = T / K;
+    ws.counters->slice_r = T % K;
+#else
     uint32_t lg = 6;
     while (lg > 0 && (T >> lg) < S * (uint64_t)PRISMDB_SLICES_PER_STREAM) --lg;
     const uint64_t K = (T + (1ull << lg) - 1) >> lg;
-    ws.counters->tasks = T;
     ws.counters->lg_tau = lg;
+#endif
+    ws.counters->tasks = T;
     // Every span one task (4 KiB blocks, log records, SST data blocks): slices
     // of tau tasks are runs of tau records, which the span kernel deals
     // without slice starts -- nslices = 0 says so and the mark pass is skipped.
@@ -1069,7 +1091,14 @@ __global__ __launch_bounds__(kPlanThreads) void crc32c_slice_mark_kernel(SpanBat
   if (K == 0) return;  // uniform batch: runs, no slice starts
   __shared__ uint64_t sh[kPlanThreads];
   const uint64_t n = batch_n(a);
+#if PRISMDB_SLICE_EXACT
+  // slice of task position x: slices 0..r-1 hold q+1 tasks, the rest q
+  const uint64_t q = ws.counters->slice_q, r = ws.counters->slice_r, rq = r * (q + 1u);
+  auto slice_of = [&](uint64_t x) -> uint64_t { return x < rq ? x / (q + 1u) : r + (x - rq) / q; };
+#else
   const uint32_t lg = ws.counters->lg_tau;
+  auto slice_of = [&](uint64_t x) -> uint64_t { return x >> lg; };
+#endif
   // Thread t walks its own per = tile/256 consecutive records of the block's
   // tile: one block scan per tile instead of one per 256 records.
   const uint64_t per = ws.tile / kPlanThreads;
@@ -1081,8 +1110,8 @@ __global__ __launch_bounds__(kPlanThreads) void crc32c_slice_mark_kernel(SpanBat
   uint64_t e = ws.bsum[blockIdx.x] + block_exclusive_scan(mine, sh, total);
   for (uint64_t i = lo; i < hi; ++i) {
     const uint32_t c = ws.cnt[i];
-    const uint64_t k1 = (e + c) >> lg;
-    for (uint64_t k = (e >> lg) + 1; k <= k1 && k <= K; ++k) ws.slice_start[k] = i + 1;
+    const uint64_t k1 = slice_of(e + c);
+    for (uint64_t k = slice_of(e) + 1; k <= k1 && k <= K; ++k) ws.slice_start[k] = i + 1;
     e += c;
   }
 }

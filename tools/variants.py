@@ -49,6 +49,8 @@ VARIANTS = {
     # span kernel: at least 64 / 256 slices per record stream (finer tail balance)
     "slices64": {"PRISMDB_SLICES_PER_STREAM": 64},
     "slices256": {"PRISMDB_SLICES_PER_STREAM": 256},
+    # task-balanced slices: ceil(T / 2^lg) of them (round 1) instead of exactly m per stream
+    "slices_pow2": {"PRISMDB_SLICE_EXACT": 0},
     # span kernel runs mode (one-task records): 16 runs per stream (round 1) / 256
     "runs16": {"PRISMDB_RUNS_PER_STREAM": 16},
     "runs256": {"PRISMDB_RUNS_PER_STREAM": 256},
