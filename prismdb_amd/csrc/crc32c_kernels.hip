@@ -83,6 +83,9 @@
 #ifndef PRISMDB_SLICE_EXACT  // task-balanced slices: exactly m per stream (1) or ceil(T / 2^lg) (0)
 #define PRISMDB_SLICE_EXACT 1
 #endif
+#ifndef PRISMDB_RUNS_EXACT  // span kernel runs: exactly m per stream (1) or runs of 2^lg records (0)
+#define PRISMDB_RUNS_EXACT 1
+#endif
 #ifndef PRISMDB_RUNS_PER_STREAM  // span kernel: runs of one-task records shrink until every stream gets this many
 #define PRISMDB_RUNS_PER_STREAM 64
 #endif
@@ -495,13 +498,33 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
   // the fixed kernel's comment has the measurement).
   const uint32_t S = 2 * nwaves;
   bool sliced = a.slice_start != nullptr;
-  uint32_t lg = 6;
   uint32_t K = sliced ? (uint32_t)const_load(a.nslices_dev, 0) : 0u;  // <= n/2 + 32 S + 2; 0: runs
+#if PRISMDB_RUNS_EXACT
+  // Runs: K = m S runs of q or q+1 records (q <= 63, runs 0..r-1 the longer),
+  // exactly m per stream; m >= PRISMDB_RUNS_PER_STREAM while runs keep >= 1
+  // record.  (Runs of 2^lg records left a stream the ceil or floor of K/S.)
+  uint32_t rq = 0, rr = 0;
+  if (K == 0) {
+    sliced = false;
+    const uint32_t rps = (uint32_t)PRISMDB_RUNS_PER_STREAM;
+    uint32_t m = (uint32_t)(((uint64_t)n + 63ull * S - 1u) / (63ull * S));
+    if (m < rps) {
+      const uint32_t mr = n / S;  // runs of >= 1 record
+      m = mr < rps ? (mr > m ? mr : m) : rps;
+    }
+    if (m < 1u) m = 1u;
+    K = (uint64_t)m * S < n ? m * S : n;
+    rq = n / K;
+    rr = n % K;
+  }
+#else
+  uint32_t lg = 6;
   if (K == 0) {
     sliced = false;
     while (lg > 0 && (n >> (lg + 1)) < nwaves * (uint32_t)PRISMDB_RUNS_PER_STREAM) --lg;
     K = (uint32_t)(((uint64_t)n + (1u << lg) - 1) >> lg);
   }
+#endif
   // Per stream: the pending record b (the one after the stream's newest task)
   // and its slice k = [lo, hi); b = n once the stream has no records left.
   struct Cursor {
@@ -514,8 +537,13 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
         lo = (uint32_t)const_load(a.slice_start, k);
         hi = (uint32_t)const_load(a.slice_start, k + 1);
       } else {
+#if PRISMDB_RUNS_EXACT
+        lo = k * rq + (k < rr ? k : rr);
+        hi = lo + rq + (k < rr ? 1u : 0u);
+#else
         lo = k << lg;
         hi = (uint32_t)((uint64_t)lo + (1u << lg) < n ? lo + (1u << lg) : n);
+#endif
       }
       hi = hi < n ? hi : n;
       if (lo < hi) {

@@ -51,6 +51,8 @@ VARIANTS = {
     "slices256": {"PRISMDB_SLICES_PER_STREAM": 256},
     # task-balanced slices: ceil(T / 2^lg) of them (round 1) instead of exactly m per stream
     "slices_pow2": {"PRISMDB_SLICE_EXACT": 0},
+    # span kernel runs of 2^lg records (before the exact partition)
+    "runs_pow2": {"PRISMDB_RUNS_EXACT": 0},
     # span kernel runs mode (one-task records): 16 runs per stream (round 1) / 256
     "runs16": {"PRISMDB_RUNS_PER_STREAM": 16},
     "runs256": {"PRISMDB_RUNS_PER_STREAM": 256},
