@@ -58,6 +58,9 @@ struct DeviceTables {
 constexpr int kQuadRounds = 5;
 constexpr uint32_t kQuadWords = 64u * kQuadRounds;   // 320 body words
 constexpr uint32_t kQuadMaxLen = 4u * kQuadWords;    // len <= 1280 B => <= 320 body words
+// A record's body-address arithmetic reaches kQuadBack bytes below its body
+// (unsigned, 32-bit offsets from the task's window base).
+constexpr uint32_t kQuadBack = kQuadMaxLen;
 
 enum : uint32_t { kRoleSpans = 0, kRoleSegments = 1 };
 

@@ -89,6 +89,9 @@
 #ifndef PRISMDB_RUNS_PER_STREAM  // span kernel: runs of one-task records shrink until every stream gets this many
 #define PRISMDB_RUNS_PER_STREAM 64
 #endif
+#ifndef PRISMDB_QUAD_CLAMPED  // quad kernel body addresses: min-clamped index per load (1) or one v_max (0)
+#define PRISMDB_QUAD_CLAMPED 0
+#endif
 #ifndef PRISMDB_QUAD_RING
 #define PRISMDB_QUAD_RING 2  // tasks in the quad kernel's ring (one folded, the rest in flight)
 #endif
@@ -1325,6 +1328,39 @@ __device__ __forceinline__ void quad_round_loads(uint32_t (&w)[kQuadRounds][4], 
   }
 }
 
+// Body word max(i + 64 M, 0) of the record whose body is at sbase + bw, with
+// ad = bw + 4 i and lo = bw - 256 M: the address is max(ad, lo) + 256 M, one
+// VALU and the load's immediate offset (a position before the body reads
+// body word 0).  ad and lo never wrap: bw >= kQuadBack (quad_window).
+template <int M>
+__device__ __forceinline__ uint32_t asm_load_word_max(const uint8_t* sbase, uint32_t ad, uint32_t lo) {
+  uint32_t r, x;
+#if PRISMDB_NT_LOADS
+  asm volatile(
+      "v_max_u32 %1, %2, %3\n\t"
+      "global_load_dword %0, %1, %4 offset:%5 nt"
+      : "=&v"(r), "=&v"(x)
+      : "v"(ad), "v"(lo), "s"(sbase), "n"(256 * M));
+#else
+  asm volatile(
+      "v_max_u32 %1, %2, %3\n\t"
+      "global_load_dword %0, %1, %4 offset:%5"
+      : "=&v"(r), "=&v"(x)
+      : "v"(ad), "v"(lo), "s"(sbase), "n"(256 * M));
+#endif
+  return r;
+}
+
+template <int M, int K>
+__device__ __forceinline__ void quad_round_loads_max(uint32_t (&w)[kQuadRounds][4], const uint8_t* sbase,
+                                                     const uint32_t (&ad)[4], const uint32_t (&lo)[kQuadRounds]) {
+  if constexpr (M < kQuadRounds) {
+    w[M][K] = asm_load_word_max<M>(sbase, ad[K], lo[M]);
+    if constexpr (K == 3) quad_round_loads_max<M + 1, 0>(w, sbase, ad, lo);
+    else quad_round_loads_max<M, K + 1>(w, sbase, ad, lo);
+  }
+}
+
 __device__ __forceinline__ uint32_t asm_load_ubyte_v(uint64_t addr) {
   uint32_t r;
   asm volatile("global_load_ubyte %0, %1, off" : "=v"(r) : "v"(addr));
@@ -1348,10 +1384,12 @@ __device__ __forceinline__ void wait_quad(uint32_t (&w)[kQuadRounds][4], uint32_
 
 // A task's window.  Its four records (4-aligned indices tb .. tb+3, those
 // below n) are read through one scalar base sb: the first short record A
-// anchors it, sb = address(A) - 8 - min(2^30, address(A) - 8), and a short
-// record is the quad kernel's if every byte it touches (log header before,
-// trailer after) lies in [sb, sb + 2^31 - 2048); any other short record is
-// listed for the generic path like a long one.  Offsets from sb then fit 31
+// anchors it, sb = address(A) - kQuadBack - min(2^30, address(A) - kQuadBack),
+// and a short record is the quad kernel's if it starts at least kQuadBack
+// bytes into the window (the body-address arithmetic reaches that far below
+// a body, unsigned) and every byte it touches (trailer after) lies below
+// sb + 2^31 - 2048; any other short record is listed for the generic path
+// like a long one.  Offsets from sb then fit 31
 // bits, so the kernel computes them in 32 bits.  The list kernel and the quad
 // kernel evaluate this same function.
 struct QuadWindow {
@@ -1370,12 +1408,12 @@ __device__ __forceinline__ QuadWindow quad_window(const uint8_t* base, const uin
   uint64_t oa = off[0];
 #pragma unroll
   for (int q = 1; q < 4; ++q) oa = A == q ? off[q] : oa;
-  const uint64_t aa = reinterpret_cast<uint64_t>(base) + oa - 8u;
+  const uint64_t aa = reinterpret_cast<uint64_t>(base) + oa - kQuadBack;
   w.sb = aa - (aa < (1ull << 30) ? aa : (1ull << 30));
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    const uint64_t d = reinterpret_cast<uint64_t>(base) + off[q] - w.sb;  // >= 8 when in the window
-    if (((sh >> q) & 1u) && d >= 8u && d < (1ull << 31) - 2048u) w.mask |= 1u << q;
+    const uint64_t d = reinterpret_cast<uint64_t>(base) + off[q] - w.sb;  // >= kQuadBack when in the window
+    if (((sh >> q) & 1u) && d >= kQuadBack && d < (1ull << 31) - 2048u) w.mask |= 1u << q;
   }
   return w;
 }
@@ -1496,14 +1534,16 @@ __global__ __launch_bounds__(kThreads) void crc32c_quad_kernel(SpanBatch a) {
     tk.u = ((uint32_t)kQuadRounds - rmax) | (mp << 4) | (fmax(8, 3u) << 8) | (fmax(10, 3u) << 10) |
            ((p0 | p1 | p2 | p3) & kQuadAnyW0) | (win.mask ? kQuadOwned : 0u);
     // Body words: frame position 64 m + v is body word 64 m + v - P, clamped
-    // into the record (the fold zeroes the words outside it).  A row without
+    // into the record (the fold zeroes the words outside it; a frame ends at
+    // its record's last body word).  A row without
     // body words reads the first body word of the first row that has some
     // (every address read is inside a record), or the zero block if none has.
     const uint32_t bo = vpo + h;  // body offset
     const uint32_t rows_w = ((p0 & 15u) ? 1u : 0u) | ((p1 & 15u) ? 2u : 0u) | ((p2 & 15u) ? 4u : 0u) |
                             ((p3 & 15u) ? 8u : 0u);
-    tk.sbase = rows_w ? tk.sb : zero;
-    const uint32_t safe = rows_w ? readlane(bo, 16u * (uint32_t)__builtin_ctz(rows_w)) : 0u;
+    // (no body words anywhere: every load reads the zero slot at bw = kQuadBack)
+    tk.sbase = rows_w ? tk.sb : zero - kQuadBack;
+    const uint32_t safe = rows_w ? readlane(bo, 16u * (uint32_t)__builtin_ctz(rows_w)) : kQuadBack;
     const uint32_t wm1 = W ? W - 1u : 0u;
     const uint32_t bw = W ? bo : safe;
     // sub-stream k's body index in round 0; opaque, so that hipcc does not
@@ -1514,7 +1554,18 @@ __global__ __launch_bounds__(kThreads) void crc32c_quad_kernel(SpanBatch a) {
       i0[k] = vlane(k) - P;
       asm volatile("" : "+v"(i0[k]));
     }
+#if PRISMDB_QUAD_CLAMPED
     quad_round_loads<0, 0>(w, tk.sbase, bw, i0, wm1);
+#else
+    // 4 + 4 address VALUs and one v_max per load (three per load clamped)
+    uint32_t ad[4], lo[kQuadRounds];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) ad[k] = bw + 4u * i0[k];
+#pragma unroll
+    for (int m = 0; m < kQuadRounds; ++m) lo[m] = bw - 256u * (uint32_t)m;
+    (void)wm1;
+    quad_round_loads_max<0, 0>(w, tk.sbase, ad, lo);
+#endif
     // Edge byte: quad 0 of the row loads head byte o (o < h), quad 1 tail
     // byte o (o < t), quad 2 stored-crc byte o (verify); the rest are masked.
     const uint32_t qd = j >> 2, o = j & 3u;

@@ -3,12 +3,14 @@ every body word and edge byte a lane loads must be a byte of a record the
 kernel owns (its body, its head/tail, the stored crc it verifies) or of the
 zero block, for any batch geometry.  A GPU fault is the failure mode this
 guards against; the model mirrors issue() step by step (window, row geometry,
-clamped body indices, the safe word of rows without body words, edge lanes).
+body addresses max(bw + 4 i, bw - 256 m) + 256 m in 32-bit unsigned
+arithmetic, the safe word of rows without body words, edge lanes).
 CPU only: no device is touched."""
 import numpy as np
 import pytest
 
-MAXLEN, QW = 1280, 320  # kQuadMaxLen, kQuadWords (crc32c_device.h)
+MAXLEN, QW, BACK = 1280, 320, 1280  # kQuadMaxLen, kQuadWords, kQuadBack (crc32c_device.h)
+M32 = 0xFFFFFFFF
 BASE = 0x7F00_0000_0000
 ZERO = 0x10_0000_0000_0000  # stands for DeviceTables::zero
 
@@ -18,12 +20,12 @@ def quad_window(base, off, ln, valid):
     if not any(sh):
         return 0, 0
     a = sh.index(True)
-    aa = base + off[a] - 8
+    aa = base + off[a] - BACK
     sb = aa - min(aa, 1 << 30)
     mask = 0
     for q in range(4):
         d = base + off[q] - sb
-        if sh[q] and 8 <= d < (1 << 31) - 2048:
+        if sh[q] and BACK <= d < (1 << 31) - 2048:
             mask |= 1 << q
     return sb, mask
 
@@ -45,19 +47,20 @@ def bad_loads(offs, lens, verify, hdr, base=BASE):
                 W = h = t = 0
             rows.append((ok, vpo, h, W, t, ln[q]))
         withw = [r[3] > 0 for r in rows]
-        sbase = sb if any(withw) else ZERO
-        safe = rows[withw.index(True)][1] + rows[withw.index(True)][2] if any(withw) else 0
+        sbase = sb if any(withw) else ZERO - BACK
+        safe = rows[withw.index(True)][1] + rows[withw.index(True)][2] if any(withw) else BACK
         bodies = [(sb + r[1] + r[2], sb + r[1] + r[2] + 4 * r[3]) for r in rows if r[0] and r[3]]
         for q, (ok, vpo, h, W, t, L) in enumerate(rows):
             p = base + off[q]
             bo = vpo + h
-            bw, wm1, P = (bo if W else safe), (W - 1 if W else 0), QW - W
+            bw, P = (bo if W else safe), QW - W
             for m in range(5):
                 for k in range(4):
                     for j in range(16):
-                        idx = (16 * (k ^ (q & 1)) + j + 64 * m - P) & 0xFFFFFFFF
-                        addr = sbase + bw + 4 * min(idx, wm1)
-                        good = sbase == ZERO and 0 <= addr - ZERO <= 12
+                        ad = (bw + 4 * (16 * (k ^ (q & 1)) + j - P)) & M32
+                        lo = (bw - 256 * m) & M32
+                        addr = sbase + max(ad, lo) + 256 * m
+                        good = sbase == ZERO - BACK and addr == ZERO
                         good = good or any(lo <= addr and addr + 4 <= hi for lo, hi in bodies)
                         bad += not good
             edges = [(p, p + L)] if ok else []
@@ -96,7 +99,7 @@ def test_window_leaves_far_and_long_records():
     row the kernel does not own must not read at base + 8 (an earlier build
     did, and faulted): the model above checks that rows without body words
     read another row's body word instead."""
-    off = np.array([100, 5 << 30, 200, 300])
+    off = np.array([1400, 5 << 30, 1600, 1800])
     lens = np.array([10, 10, 100_000, 20])
     sb, mask = quad_window(BASE, list(off), list(lens), 15)
     assert mask == 0b1001

@@ -44,6 +44,8 @@ VARIANTS = {
     "quad_nomask": {"PRISMDB_QUAD_NOMASK": 1},
     "quad_ra2": {"PRISMDB_QUAD_RALIGN_GROUPS": 2},
     "quad_ra1": {"PRISMDB_QUAD_RALIGN_GROUPS": 1},
+    # quad kernel body loads: three address VALUs per load (clamped index)
+    "quad_clamped": {"PRISMDB_QUAD_CLAMPED": 1},
     # every descriptor batch through the quad kernel first
     "quad_all": {"PRISMDB_QUAD_DEFAULT": 1},
     # span kernel: at least 64 / 256 slices per record stream (finer tail balance)
