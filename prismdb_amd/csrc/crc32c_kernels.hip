@@ -56,6 +56,9 @@
 #ifndef PRISMDB_XOR3
 #define PRISMDB_XOR3 1  // three-input XORs through v_bitop3_b32
 #endif
+#ifndef PRISMDB_SPAN_INJ_RING  // span kernel: initial register written into the ring registers (1) or folded in (0)
+#define PRISMDB_SPAN_INJ_RING 1
+#endif
 #ifndef PRISMDB_SPAN_J0  // measurement knob: span kernel folds rounds >= this only (wrong results)
 #define PRISMDB_SPAN_J0 0
 #endif
@@ -651,12 +654,16 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
   // Start of a chunk: the initial register (chunk 0), already fed the head
   // bytes by the planner.  It enters with body word 0: lane pad%64 of round
   // J = pad/64, a wave-uniform index.  J = 0 (full chunks, pads < 64) is one
-  // XOR; otherwise a rarely taken block puts it into round J's word under a
-  // scalar mask (v_bitop3 w ^ (inj & m)), no branches per round.  (A 16-way
-  // switch on J compiled to a compare tree with register copies at its merges
-  // that every task walked; an indexed w[J] made hipcc move the ring to
-  // scratch.)  kRoundSkip (log records) returns inj and J instead: its fold tests
-  // every round anyway and masks only the 4-5 rounds it folds.
+  // XOR; otherwise a block puts it into round J's word under a scalar mask
+  // (v_bitop3 w ^ (inj & m)), no branches per round.  hipcc copies the 16 ring
+  // registers out and back around that block on the common path (30 v_mov per
+  // span).  PRISMDB_SPAN_INJ_RING 0 returns (inj, J) instead and folds it in
+  // (a second copy of the round loop under masks, as kRoundSkip does): no
+  // copies, but no faster either (4 KiB descriptors +0.4 %, config-3 mix
+  // -1.1 %, profiles/r02v_variants_span_injection.json): the span kernel is
+  // not bound by its VALU count.  (A 16-way switch on J compiled to a compare
+  // tree with copies at its merges; an indexed w[J] made hipcc move the ring
+  // to scratch.)
   auto begin = [&](int s, const Task& t, uint32_t (&w)[kR], uint32_t& Jout) -> uint32_t {
     Jout = 0;
     if (t.c != 0) return 0u;
@@ -665,9 +672,9 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
     acc[s] = 0u;
     if (t.r.z == 0) return 0u;
     const uint32_t pad = t.pad();
-    const uint32_t inj = lane == (pad & 63u) ? rr : 0u;
     const uint32_t J = PRISMDB_SPAN_INJ0 ? 0u : pad >> 6;
-    if (kRoundSkip) {
+    const uint32_t inj = lane == (pad & 63u) ? rr : 0u;
+    if (!PRISMDB_SPAN_INJ_RING || kRoundSkip) {
       Jout = J;
       return inj;
     }
@@ -675,10 +682,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
       w[0] ^= inj;
     } else {
 #pragma unroll
-      for (int j = 1; j < kR; ++j) {
-        const uint32_t m = (uint32_t)j == J ? ~0u : 0u;
-        w[j] = __builtin_amdgcn_bitop3_b32(w[j], inj, m, 0x78);
-      }
+      for (int j = 1; j < kR; ++j) w[j] = __builtin_amdgcn_bitop3_b32(w[j], inj, (uint32_t)j == J ? ~0u : 0u, 0x78);
     }
     return 0u;
   };
@@ -710,7 +714,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
   // Fold the pair (stream 0 task tx in wx, stream 1 task ty in wy).
   auto fold = [&](const Task& tx, uint32_t (&wx)[kR], uint32_t ex, const Task& ty,
                   uint32_t (&wy)[kR], uint32_t ey) {
-    uint32_t Jx = 0, Jy = 0, ix = 0, iy = 0;  // kRoundSkip: injections applied in the fold
+    uint32_t Jx = 0, Jy = 0, ix = 0, iy = 0;  // injections (register into round J's word)
     if (!tx.skip()) ix = begin(0, tx, wx, Jx);
     if (!ty.skip()) iy = begin(1, ty, wy, Jy);
     uint32_t ax = acc[0], ay = acc[1];
@@ -726,16 +730,15 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
     };
     const uint32_t fx = first_round(tx), fy = first_round(ty);
     const uint32_t j0 = kRoundSkip ? (fx < fy ? fx : fy) : 0u;
-    if (!kRoundSkip || (j0 == 0 && (Jx | Jy) == 0)) {
-      // kRoundSkip: both registers enter in round 0 (ix = iy = 0 otherwise); the
-      // ring registers themselves are left untouched
+    if ((PRISMDB_SPAN_INJ_RING && !kRoundSkip) || (j0 == 0 && (Jx | Jy) == 0)) {
+      // both registers enter in round 0; the ring registers are left untouched
 #pragma unroll
       for (int j = PRISMDB_SPAN_J0; j < kR; ++j) {
         ax = step256(lds, tab, ax, j == 0 ? wx[0] ^ ix : wx[j]);
         ay = step256(lds, tab, ay, j == 0 ? wy[0] ^ iy : wy[j]);
       }
     } else {
-      // kRoundSkip with a padded chunk 0: rounds before j0 skipped, round j's word
+      // a padded chunk 0: rounds before j0 skipped (kRoundSkip), round j's word
       // takes the injection under a scalar mask (one v_bitop3 w ^ (inj & m))
 #pragma unroll
       for (int j = 0; j < kR; ++j) {

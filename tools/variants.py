@@ -46,6 +46,8 @@ VARIANTS = {
     "quad_ra1": {"PRISMDB_QUAD_RALIGN_GROUPS": 1},
     # quad kernel body loads: three address VALUs per load (clamped index)
     "quad_clamped": {"PRISMDB_QUAD_CLAMPED": 1},
+    # span kernel: initial register folded in (no ring-register copies at the merge)
+    "inj_fold": {"PRISMDB_SPAN_INJ_RING": 0},
     # every descriptor batch through the quad kernel first
     "quad_all": {"PRISMDB_QUAD_DEFAULT": 1},
     # span kernel: at least 64 / 256 slices per record stream (finer tail balance)
