@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Headline benchmark: batched CRC32C over device-resident 4 KiB SST blocks.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--nblocks B] [--e2e]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--nblocks B] [--strong] [--no-gather] [--e2e]
 
 Workload (BASELINE.json configs[1], "config 2"): per GPU, 16 Mi blocks x 4096 B
 (64 GiB) generated on the device from the splitmix64 stream, stride 4096,
@@ -10,7 +10,9 @@ base 256-B aligned.  One step = one pass of the engine over the whole batch
 RCCL gather of the 4-byte results to rank 0 (overlapped with the next pass on
 RCCL's own stream; the last one is inside the timed region).
 N > 1 runs one process per GPU under torch.distributed.run (weak scaling: each
-rank owns a different 64 GiB slice of the global block stream).
+rank owns a different 64 GiB slice of the global block stream).  --strong keeps
+the total fixed instead (--nblocks blocks in all, nblocks / N per rank; SURVEY
+8(d) config 5), and --no-gather drops the RCCL gather (config 5 asks for both).
 
 Printed (rank 0): ONE JSON line with the driver's contract fields plus
   roofline      dominant kernel vs the HBM roofline (HIP events on the launch stream)
@@ -44,7 +46,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--nblocks", type=int, default=1 << 24, help="4 KiB blocks per GPU")
+    ap.add_argument("--nblocks", type=int, default=1 << 24, help="4 KiB blocks per GPU (--strong: in total)")
+    ap.add_argument("--strong", action="store_true", help="strong scaling: --nblocks is the total over all ranks")
+    ap.add_argument("--no-gather", action="store_true", help="N > 1: no RCCL gather of the results")
     ap.add_argument("--cpu-sample-blocks", type=int, default=1 << 18)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-seconds of reference work")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -270,6 +274,11 @@ def main() -> int:
 
     crc32c.device_init(local)
     nblk = args.nblocks
+    if args.strong:
+        if args.nblocks % world:
+            raise SystemExit(f"--strong: --nblocks {args.nblocks} is not a multiple of {world} ranks")
+        nblk = args.nblocks // world
+    gather = world > 1 and not args.no_gather
     shard = ShardedBatch(nblocks_per_rank=nblk, block_bytes=BLOCK, rank=rank, world=world, device=dev)
     buf = torch.empty(nblk * BLOCK, dtype=torch.uint8, device=dev)
     crc32c.fill_synthetic(buf, SEED, byte_offset=shard.first_block * BLOCK)
@@ -290,7 +299,7 @@ def main() -> int:
         crc32c.batch_fixed(buf, BLOCK, BLOCK, nblk, out=outs[slot])
         if timed:
             ev[i][1].record(stream)
-        if world > 1:
+        if gather:
             pending[slot] = shard.gather_async(outs[slot], slot)
 
     for i in range(args.warmup):
@@ -327,7 +336,7 @@ def main() -> int:
     achieved = algo_bytes / (kern_ms / 1e3) / 1e9
     # rank-0 results check: gathered results of the last step hold every rank's shard
     gathered_ok = None
-    if world > 1:
+    if gather:
         gathered_ok = shard.check_gathered(outs[(args.steps - 1) % 2])
 
     cpu = None
@@ -346,17 +355,19 @@ def main() -> int:
             "warmup": args.warmup,
             "ms_per_step": round(elapsed * 1e3 / args.steps, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.strong else "weak",
             "vs_baseline": None,
             "dtype": "u32",
             "data": "synthetic (device-generated splitmix64 stream, regenerable on host)",
             "config": {
                 "workload": "config2: 16Mi x 4096 B blocks per GPU, stride 4096, device-resident (BASELINE.json configs[1])"
-                if nblk == 1 << 24 else f"{nblk} x 4096 B blocks per GPU, stride 4096, device-resident",
+                if nblk == 1 << 24 and not args.strong else
+                (f"config5 strong scaling: {args.nblocks} x 4096 B blocks in total, {nblk} per GPU, stride 4096, "
+                 "device-resident" if args.strong else f"{nblk} x 4096 B blocks per GPU, stride 4096, device-resident"),
                 "blocks_per_gpu": nblk,
                 "block_bytes": BLOCK,
                 "bytes_per_gpu": nblk * BLOCK,
-                "parallelism": f"shard{world}" + ("+rccl_gather" if world > 1 else ""),
+                "parallelism": f"shard{world}" + ("+rccl_gather" if gather else ""),
             },
             "roofline": {
                 "bound": "hbm",

@@ -59,6 +59,9 @@
 #ifndef PRISMDB_SPAN_INJ_RING  // span kernel: initial register written into the ring registers (1) or folded in (0)
 #define PRISMDB_SPAN_INJ_RING 1
 #endif
+#ifndef PRISMDB_SPAN_REC_WAIT  // measurement knob: span kernel waits for each record read at once
+#define PRISMDB_SPAN_REC_WAIT 0
+#endif
 #ifndef PRISMDB_SPAN_J0  // measurement knob: span kernel folds rounds >= this only (wrong results)
 #define PRISMDB_SPAN_J0 0
 #endif
@@ -604,6 +607,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
         pend[s] = read_rec(cur[s].b);
       }
     }
+    if (PRISMDB_SPAN_REC_WAIT) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   };
   // 17 loads, always.
   auto issue = [&](const Task& t, uint32_t (&w)[kR], uint32_t& e) {

@@ -48,6 +48,8 @@ VARIANTS = {
     "quad_clamped": {"PRISMDB_QUAD_CLAMPED": 1},
     # span kernel: initial register folded in (no ring-register copies at the merge)
     "inj_fold": {"PRISMDB_SPAN_INJ_RING": 0},
+    # measurement-only: span kernel waits for every record's scalar read right away
+    "rec_wait": {"PRISMDB_SPAN_REC_WAIT": 1},
     # every descriptor batch through the quad kernel first
     "quad_all": {"PRISMDB_QUAD_DEFAULT": 1},
     # span kernel: at least 64 / 256 slices per record stream (finer tail balance)
