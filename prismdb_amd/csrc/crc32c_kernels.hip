@@ -62,6 +62,12 @@
 #ifndef PRISMDB_SPAN_REC_WAIT  // measurement knob: span kernel waits for each record read at once
 #define PRISMDB_SPAN_REC_WAIT 0
 #endif
+#ifndef PRISMDB_FIXED_DUMMY_SALU  // measurement knob: fixed kernel issues this many extra SALU per span pair
+#define PRISMDB_FIXED_DUMMY_SALU 0
+#endif
+#ifndef PRISMDB_FIXED_DUMMY_VALU  // measurement knob: ... and this many extra VALU per span pair
+#define PRISMDB_FIXED_DUMMY_VALU 0
+#endif
 #ifndef PRISMDB_SPAN_J0  // measurement knob: span kernel folds rounds >= this only (wrong results)
 #define PRISMDB_SPAN_J0 0
 #endif
@@ -915,6 +921,19 @@ __global__ __launch_bounds__(kThreads) void crc32c_fixed_kernel(SpanBatch a) {
 #endif
     const uint32_t ca = wave_xor(va) ^ kConditioning, cb = wave_xor(vb) ^ kConditioning;
     const uint32_t i = (uint32_t)(cur & (kRun - 1u));  // the pair's lanes in the run
+#if PRISMDB_FIXED_DUMMY_SALU
+    {  // sensitivity probe: a dependent chain of scalar ALU work
+      uint32_t d = i;
+      asm volatile(".rept %1\n\ts_xor_b32 %0, %0, 0x5a5a\n\t.endr" : "+s"(d) : "n"(PRISMDB_FIXED_DUMMY_SALU));
+    }
+#endif
+#if PRISMDB_FIXED_DUMMY_VALU
+    {  // sensitivity probe: vector ALU work, four independent chains
+      uint32_t d0 = lane, d1 = lane + 1u, d2 = lane + 2u, d3 = lane + 3u;
+      asm volatile(".rept %4\n\tv_xor_b32 %0, 0x5a5a, %0\n\tv_xor_b32 %1, 0x5a5a, %1\n\tv_xor_b32 %2, 0x5a5a, %2\n\tv_xor_b32 %3, 0x5a5a, %3\n\t.endr"
+                   : "+v"(d0), "+v"(d1), "+v"(d2), "+v"(d3) : "n"(PRISMDB_FIXED_DUMMY_VALU / 4));
+    }
+#endif
     res = lane == i ? (masked ? mask_crc(ca) : ca) : res;
     res = lane == i + 1u ? (masked ? mask_crc(cb) : cb) : res;
     if (kVerify) {

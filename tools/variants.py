@@ -50,6 +50,9 @@ VARIANTS = {
     "inj_fold": {"PRISMDB_SPAN_INJ_RING": 0},
     # measurement-only: span kernel waits for every record's scalar read right away
     "rec_wait": {"PRISMDB_SPAN_REC_WAIT": 1},
+    # measurement-only: fixed kernel with extra SALU / VALU per span pair (issue sensitivity)
+    "salu200": {"PRISMDB_FIXED_DUMMY_SALU": 200},
+    "valu64": {"PRISMDB_FIXED_DUMMY_VALU": 64},
     # every descriptor batch through the quad kernel first
     "quad_all": {"PRISMDB_QUAD_DEFAULT": 1},
     # span kernel: at least 64 / 256 slices per record stream (finer tail balance)
