@@ -68,6 +68,12 @@
 #ifndef PRISMDB_FIXED_DUMMY_VALU  // measurement knob: ... and this many extra VALU per span pair
 #define PRISMDB_FIXED_DUMMY_VALU 0
 #endif
+#ifndef PRISMDB_SPAN_WG_EXIT  // span kernel: groups without a stream leave before the table load
+#define PRISMDB_SPAN_WG_EXIT 1
+#endif
+#ifndef PRISMDB_PLAN_SERIAL_SEG  // A/B knob: a long span's thread writes all its segment records itself
+#define PRISMDB_PLAN_SERIAL_SEG 0
+#endif
 #ifndef PRISMDB_SPAN_J0  // measurement knob: span kernel folds rounds >= this only (wrong results)
 #define PRISMDB_SPAN_J0 0
 #endif
@@ -483,15 +489,8 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
     skip_long = false;
   }
   if (n == 0) return;
-
-  __shared__ uint32_t lds[kLdsWords];
   const uint32_t tid = threadIdx.x;
-  load_tables(lds, a.tabs, tid);
   const uint32_t lane = tid & 63u;
-  __syncthreads();
-  const StrideLanes tab = stride_lanes(lane);
-  const uint32_t nibtab = 4u * (kTabWords + lane);  // byte address of lane's nibble entry [0][0]
-  const ShortShift ss = short_shift_cols(lane);
   const uint32_t wave = rfl(blockIdx.x * kWavesPerGroup + (tid >> 6));
   const uint32_t nwaves = gridDim.x * kWavesPerGroup;
   // Schedule.  The records are cut into slices of consecutive records, and
@@ -540,6 +539,17 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
     K = (uint32_t)(((uint64_t)n + (1u << lg) - 1) >> lg);
   }
 #endif
+  // A group whose streams (2 per wave) are all >= K has no slice or run: it
+  // leaves before loading the tables (the segment pass of a batch with a few
+  // long spans launches the whole grid for a handful of streams).
+  if (PRISMDB_SPAN_WG_EXIT && blockIdx.x * 2u * kWavesPerGroup >= K) return;
+
+  __shared__ uint32_t lds[kLdsWords];
+  load_tables(lds, a.tabs, tid);
+  __syncthreads();
+  const StrideLanes tab = stride_lanes(lane);
+  const uint32_t nibtab = 4u * (kTabWords + lane);  // byte address of lane's nibble entry [0][0]
+  const ShortShift ss = short_shift_cols(lane);
   // Per stream: the pending record b (the one after the stream's newest task)
   // and its slice k = [lo, hi); b = n once the stream has no records left.
   struct Cursor {
@@ -1025,7 +1035,15 @@ __global__ __launch_bounds__(kPlanThreads) void crc32c_plan_kernel(SpanBatch a, 
   if (threadIdx.x == 0) sum = 0;
   __syncthreads();
   uint32_t mine = 0;  // <= tile/256 spans of <= 32 tasks each
-  for (uint64_t i = lo + threadIdx.x; i < hi; i += kPlanThreads) {
+  // Uniform trip count (the block's bounds), so the wave can write a long
+  // span's segment records together below.
+  for (uint64_t i0 = lo; i0 < hi; i0 += kPlanThreads) {
+    const uint64_t i = i0 + threadIdx.x;
+    // this lane's long span, if it has one, for the wave's segment writes
+    const uint8_t* sp = nullptr;
+    uint64_t spos = 0;
+    uint32_t snseg = 0, sfirst = 0, sinit = 0;
+    if (i < hi) do {
     const uint64_t q = a.idx != nullptr ? a.idx[i] : i;  // the caller's span
     const uint64_t off = kDesc ? a.off[q] : q * a.stride;
     const uint32_t len = kDesc ? a.len[q] : a.len_c;
@@ -1038,22 +1056,49 @@ __global__ __launch_bounds__(kPlanThreads) void crc32c_plan_kernel(SpanBatch a, 
     const uint32_t cnt = lng ? 1u : (r.z ? (r.z + (1u << lgb) - 1u) >> lgb : 1u);  // Task::nch()
     ws.cnt[i] = cnt;
     mine += cnt;
-    if (!lng) continue;
+    if (!lng) break;
     const uint32_t nseg = (len + kSegment - 1u) / kSegment;
     const uint32_t first = len - (nseg - 1u) * kSegment;
     const uint64_t pos = atomicAdd((unsigned long long*)&ws.counters->nseg, (unsigned long long)nseg);
     const uint32_t li = atomicAdd(&ws.counters->nlong, 1u);
     if (pos + nseg > ws.cap_seg || li >= ws.cap_long) {
       atomicOr(&ws.counters->overflow, 1u);
-      continue;
+      break;
     }
     ws.long_span[li] = i;
     ws.long_first[li] = pos;
     ws.long_nseg[li] = nseg;
-    // segments: the general kernel (4 KiB chunks) folds them
-    ws.seg_rec[pos] = make_rec(p, first, init, false, 10u);
-    for (uint32_t s = 1; s < nseg; ++s)
-      ws.seg_rec[pos + s] = make_rec(p + first + (uint64_t)(s - 1u) * kSegment, kSegment, kConditioning, false, 10u);
+    sp = p;
+    spos = pos;
+    snseg = nseg;
+    sfirst = first;
+    sinit = init;
+    } while (false);
+    // Segments: the general kernel (4 KiB chunks) folds them.  Their records
+    // are written by the whole wave, one long span at a time, 64 segments per
+    // step: each record's head bytes are a dependent global read, and one
+    // thread writing a 487 KB index span's 15 records took 12 us per call
+    // (the planner's whole time on one SST file).
+#if PRISMDB_PLAN_SERIAL_SEG
+    if (sp != nullptr) {
+      ws.seg_rec[spos] = make_rec(sp, sfirst, sinit, false, 10u);
+      for (uint32_t s = 1; s < snseg; ++s)
+        ws.seg_rec[spos + s] = make_rec(sp + sfirst + (uint64_t)(s - 1u) * kSegment, kSegment, kConditioning, false, 10u);
+    }
+#else
+    uint64_t lm = __ballot(sp != nullptr);
+    while (lm != 0u) {
+      const int src = __ffsll((long long)lm) - 1;
+      lm &= lm - 1u;
+      const uint8_t* bp = reinterpret_cast<const uint8_t*>(__shfl((unsigned long long)(uintptr_t)sp, src, 64));
+      const uint64_t bpos = __shfl((unsigned long long)spos, src, 64);
+      const uint32_t bn = __shfl(snseg, src, 64), bf = __shfl(sfirst, src, 64), bi = __shfl(sinit, src, 64);
+      for (uint32_t s = threadIdx.x & 63u; s < bn; s += 64u)
+        ws.seg_rec[bpos + s] = s == 0u ? make_rec(bp, bf, bi, false, 10u)
+                                       : make_rec(bp + bf + (uint64_t)(s - 1u) * kSegment, kSegment, kConditioning,
+                                                  false, 10u);
+    }
+#endif
   }
   atomicAdd(&sum, (unsigned long long)mine);
   __syncthreads();

@@ -52,6 +52,10 @@ VARIANTS = {
     "rec_wait": {"PRISMDB_SPAN_REC_WAIT": 1},
     # measurement-only: fixed kernel with extra SALU / VALU per span pair (issue sensitivity)
     "salu200": {"PRISMDB_FIXED_DUMMY_SALU": 200},
+    # span kernel: every group loads the tables, streams or not (as in round 1)
+    "no_wg_exit": {"PRISMDB_SPAN_WG_EXIT": 0},
+    # planner: a long span's thread writes its segment records alone (as in round 1)
+    "plan_serial": {"PRISMDB_PLAN_SERIAL_SEG": 1},
     "valu64": {"PRISMDB_FIXED_DUMMY_VALU": 64},
     # every descriptor batch through the quad kernel first
     "quad_all": {"PRISMDB_QUAD_DEFAULT": 1},
@@ -146,6 +150,13 @@ def do_run(args, names):
     al = rng.integers(0, 70000, size=(args.gib << 30) // 35000 // 2).astype(np.int64)
     ao = np.sort(rng.integers(0, (args.gib << 30) // 2 - 70001, size=len(al))).astype(np.int64)
     aoff, alen = torch.from_numpy(ao).to(dev), torch.from_numpy(al.astype(np.int32)).to(dev)
+    # one SST file's worth (16 811 data blocks + the 486 977-B index span), the
+    # granularity a compaction verifies at: per-call latency, 50 calls per timing
+    nfd = 16811
+    foff = torch.from_numpy(np.concatenate([np.arange(nfd, dtype=np.int64) * 3992, [nfd * 3992]])).to(dev)
+    flen = torch.from_numpy(np.concatenate([np.full(nfd, 3988, dtype=np.int32), [486977]]).astype(np.int32)).to(dev)
+    fout = torch.empty(nfd + 1, dtype=torch.int32, device=dev)
+    calls = {"file_fixed": 50, "file_desc": 50}
     work = {
         "fixed4k": (lambda n: libs[n][0](buf.data_ptr(), 4096, 4096, nblk, 0, out.data_ptr(), None, 0, sp),
                     nblk * 4100),
@@ -164,20 +175,25 @@ def do_run(args, names):
                                          hout.data_ptr(), None, 0, sp), nh * ((64 << 20) - 5 + 16)),
         "adversarial": (lambda n: libs[n][1](buf.data_ptr(), aoff.data_ptr(), alen.data_ptr(), None, len(al),
                                              out.data_ptr(), None, 0, sp), int(al.sum()) + 16 * len(al)),
+        "file_fixed": (lambda n: libs[n][0](buf.data_ptr(), 3992, 3988, nfd, 0, fout.data_ptr(), None, 0, sp),
+                       nfd * (3988 + 4)),
+        "file_desc": (lambda n: libs[n][1](buf.data_ptr(), foff.data_ptr(), flen.data_ptr(), None, nfd + 1,
+                                           fout.data_ptr(), None, 0, sp), nfd * (3988 + 16) + 486977 + 16),
     }
 
-    def timed(fn, n):
+    def timed(fn, n, k=1):  # mean of k back-to-back calls
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(stream)
-        rc = fn(n)
+        for _ in range(k):
+            rc = fn(n)
+            assert rc == 0, (n, rc)
         e1.record(stream)
         e1.synchronize()
-        assert rc == 0, (n, rc)
-        return e0.elapsed_time(e1) / 1e3
+        return e0.elapsed_time(e1) / 1e3 / k
 
     res = {w: {n: [] for n in names} for w in work}
     agree = {}
-    outs_of = {"wal": wout, "sst3988": sout, "huge64m": hout}
+    outs_of = {"wal": wout, "sst3988": sout, "huge64m": hout, "file_fixed": fout, "file_desc": fout}
     for w, (fn, _) in work.items():
         ref = None
         for n in names:
@@ -198,10 +214,10 @@ def do_run(args, names):
     for rep in range(args.reps):
         for w, (fn, _) in work.items():
             for n in (names if rep % 2 == 0 else names[::-1]):
-                res[w][n].append(timed(fn, n))
+                res[w][n].append(timed(fn, n, calls.get(w, 1)))
     print(json.dumps({"gib": args.gib, "reps": args.reps, "agree": agree,
                       "results": {w: {n: {"GB/s_median": round(work[w][1] / statistics.median(v) / 1e9, 1),
-                                          "ms_median": round(statistics.median(v) * 1e3, 3)}
+                                          "ms_median": round(statistics.median(v) * 1e3, 4)}
                                       for n, v in r.items()} for w, r in res.items()}}, indent=1))
 
 
