@@ -452,7 +452,10 @@ struct Task {
   __device__ uint32_t h() const { return (r.y >> 26) & 3u; }
   __device__ uint32_t t() const { return (r.y >> 28) & 3u; }
   __device__ bool lng() const { return (r.y >> 30) & 1u; }
-  __device__ uint32_t nch(uint32_t lgb) const { return r.z ? (r.z + (1u << lgb) - 1u) >> lgb : 1u; }
+  // ceil(z / chunk) without the 32-bit wrap of z + chunk - 1 (z up to 2^32 - 4)
+  __device__ uint32_t nch(uint32_t lgb) const {
+    return r.z ? (r.z >> lgb) + ((r.z & ((1u << lgb) - 1u)) != 0u ? 1u : 0u) : 1u;
+  }
   __device__ uint32_t len() const { return h() + r.z + t(); }
   __device__ const uint8_t* start() const { return body() - h(); }
 };
@@ -629,11 +632,17 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
   auto issue = [&](const Task& t, uint32_t (&w)[kR], uint32_t& e) {
     const bool live = !t.skip();
     const uint32_t pad = t.pad(), h = t.h(), tl = t.t(), nch = t.nch(kLgB), len = t.len();
-    // Edge window: [start - hb, start + len + 4) when verifying a trailer after
-    // the span, [start - 6, start + len) when the stored crc is a log header.
-    const uint32_t hb = kVerify && hdr ? kLogCrcBack : 0u;
+    // Edge window: the tail bytes and the stored trailer after them, [body
+    // end, + t + 4); with a log header, [start - 6, start + len) (the stored
+    // crc lies before the span).  Sizes and offsets saturate at 2^32 - 1: only
+    // a log-header span of more than 2^32 - 10 bytes (log records are <= 32 KiB)
+    // would lose its tail bytes, and only if it is folded here at all (long
+    // spans go through segments unless the segment workspace overflows).
+    const bool hwin = kVerify && hdr;
+    auto sat = [](uint64_t x) -> uint32_t { return x > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)x; };
     u32x4 rb = buffer_rsrc(t.body(), live ? t.r.z : 0u);
-    u32x4 re = buffer_rsrc(t.start() - hb, live ? hb + len + (kVerify && !hdr ? 4u : 0u) : 0u);
+    u32x4 re = buffer_rsrc(hwin ? t.start() - kLogCrcBack : t.body() + t.r.z,
+                           live ? (hwin ? sat((uint64_t)kLogCrcBack + len) : tl + (kVerify ? 4u : 0u)) : 0u);
     // A VALU write of an SGPR (v_readfirstlane) read by a VMEM instruction
     // needs 5 wait states, and hipcc inserts none before inline asm
     // (cdna_hip_programming.md 5.7 item 2).  The descriptors are built from
@@ -663,8 +672,9 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
     // Edge bytes of the last chunk: tail bytes (lanes 3-5), stored crc (6-9).
     const bool last = t.c + 1 == nch;
     uint32_t eoff = 0xFFFFFFFFu;
-    if (last && lane >= 3u && lane < 3u + tl) eoff = hb + h + t.r.z + (lane - 3u);
-    if (kVerify && last && lane >= 6u && lane < 10u) eoff = (hdr ? 0u : len) + (lane - 6u);
+    if (last && lane >= 3u && lane < 3u + tl)
+      eoff = hwin ? sat((uint64_t)kLogCrcBack + h + t.r.z + (lane - 3u)) : lane - 3u;
+    if (kVerify && last && lane >= 6u && lane < 10u) eoff = (hwin ? 0u : tl) + (lane - 6u);
     e = buf_ubyte(re, eoff);
   };
 
@@ -1053,11 +1063,11 @@ __global__ __launch_bounds__(kPlanThreads) void crc32c_plan_kernel(SpanBatch a, 
     const SpanRec r = make_rec(p, len, init, lng, a.chunk_lg);
     ws.rec[i] = r;
     const uint32_t lgb = a.chunk_lg + 2u;
-    const uint32_t cnt = lng ? 1u : (r.z ? (r.z + (1u << lgb) - 1u) >> lgb : 1u);  // Task::nch()
+    const uint32_t cnt = lng ? 1u : (r.z ? (r.z >> lgb) + ((r.z & ((1u << lgb) - 1u)) != 0u ? 1u : 0u) : 1u);  // Task::nch()
     ws.cnt[i] = cnt;
     mine += cnt;
     if (!lng) break;
-    const uint32_t nseg = (len + kSegment - 1u) / kSegment;
+    const uint32_t nseg = (uint32_t)(((uint64_t)len + kSegment - 1u) / kSegment);  // len up to 2^32 - 1
     const uint32_t first = len - (nseg - 1u) * kSegment;
     const uint64_t pos = atomicAdd((unsigned long long*)&ws.counters->nseg, (unsigned long long)nseg);
     const uint32_t li = atomicAdd(&ws.counters->nlong, 1u);

@@ -185,6 +185,48 @@ def test_huge_span_split_path(dev, oracle):
     _check_spans(dev, oracle, host, [3, 17, (40 << 20) + 5], [40 << 20, 131073, 4000])
 
 
+def test_max_length_span(dev, oracle):
+    """The longest span a descriptor holds (len = 2^32 - 1) at an odd offset,
+    with an initial value, Mask and VERIFY against its stored trailer, next to
+    a short span with a damaged trailer: the split path's 131 072 segments and
+    their combine, against the oracle on host-regenerated bytes.  (The
+    planner's segment and task counts wrapped in 32 bits for spans within
+    32 KiB of 2^32.)"""
+    import torch
+    from prismdb_amd import crc32c
+
+    L = 0xFFFFFFFF
+    off = np.array([5, 5 + L + 4], dtype=np.uint64)
+    lens = np.array([L, 1000], dtype=np.uint32)
+    size = int(off[1]) + 1000 + 4 + 3
+    free, _ = torch.cuda.mem_get_info()
+    if free < size + (2 << 30):
+        pytest.skip("not enough device memory for a 4 GiB span")
+    seed = 0x5EED0031
+    host = oracle.synth(size, seed)
+    init = np.array([0x9E3779B9, 0x01234567], dtype=np.uint32)
+    raw, _ = oracle.batch(host, off, lens, init)  # one pass over the 4 GiB (no trailer inside a span)
+    want = np.array([oracle.mask(int(c)) for c in raw], dtype=np.uint32)
+    for i, bad in ((0, 0), (1, 1)):
+        t = int(off[i]) + int(lens[i])
+        host[t:t + 4] = np.frombuffer(np.uint32(int(want[i]) ^ bad).tobytes(), dtype=np.uint8)
+    buf = torch.empty(size, dtype=torch.uint8, device=dev)
+    crc32c.fill_synthetic(buf, seed)
+    for i in range(2):
+        t = int(off[i]) + int(lens[i])
+        buf[t:t + 4] = torch.from_numpy(host[t:t + 4].copy()).to(dev)
+    d_off = torch.from_numpy(off.astype(np.int64)).to(dev)
+    d_len = torch.from_numpy(lens.view(np.int32).copy()).to(dev)
+    d_init = torch.from_numpy(init.view(np.int32).copy()).to(dev)
+    out, mm = crc32c.batch(buf, d_off, d_len, d_init, mask=True, verify=True)
+    np.testing.assert_array_equal(_u32(out), want)
+    assert mm.cpu().numpy().tolist() == [0, 1]
+    out2, _ = crc32c.batch(buf, d_off[:1], d_len[:1], d_init[:1])  # unmasked, no verify
+    assert int(_u32(out2)[0]) == int(raw[0])
+    del buf, out, mm, out2
+    torch.cuda.empty_cache()
+
+
 @pytest.mark.parametrize("uniform", [False, True])
 def test_long_spans_close_slices(dev, oracle, uniform):
     """300 000 short spans with long (split-path) spans at positions 63 mod 64
