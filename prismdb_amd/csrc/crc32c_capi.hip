@@ -32,6 +32,10 @@ using prismdb::dev::SplitCounters;
 using prismdb::dev::SplitWs;
 
 thread_local std::string t_last_error;
+// The calling thread's last descriptor batch: its split counters and stream
+// (read back only by the test hook prismdb_crc32c_last_split).
+thread_local const prismdb::dev::SplitCounters* t_last_counters = nullptr;
+thread_local hipStream_t t_last_stream = nullptr;
 
 int Fail(int code, const std::string& msg) {
   t_last_error = msg;
@@ -332,6 +336,8 @@ int RunBatch(DeviceCtx& ctx, const SpanBatch& base_args, bool desc, bool verify,
   if (rc != 0) return rc;
   hipError_t e = hipMemsetAsync(ws.counters, 0, sizeof(SplitCounters), s);
   if (e != hipSuccess) return FailHip(e, "hipMemsetAsync");
+  t_last_counters = ws.counters;
+  t_last_stream = s;
   uint32_t* const caller_out = a.out;
   uint8_t* const caller_mm = a.mismatch;
   if (quad) {
@@ -466,5 +472,22 @@ void prismdb_crc32c_force_generic(int on) { g_force_generic = on != 0; }
 // (0 = log-record batches, the default; 1 = every batch; -1 = none), so the
 // parity tests and the A/B harness can pin either path.
 void prismdb_crc32c_quad_mode(int mode) { g_quad_mode = mode > 0 ? 1 : (mode < 0 ? -1 : 0); }
+
+// Not in the public header: the split counters of the calling thread's last
+// descriptor batch {long spans, segments, overflow flag, spans listed by the
+// quad kernel}, after waiting for its stream, so the tests can tell which
+// path a batch took.  Returns 0, or -1 if the thread has run no such batch.
+int prismdb_crc32c_last_split(uint64_t out[4]) {
+  if (t_last_counters == nullptr) return -1;
+  prismdb::dev::SplitCounters c{};
+  hipError_t e = hipStreamSynchronize(t_last_stream);
+  if (e == hipSuccess) e = hipMemcpy(&c, t_last_counters, sizeof(c), hipMemcpyDeviceToHost);
+  if (e != hipSuccess) return FailHip(e, "prismdb_crc32c_last_split");
+  out[0] = c.nlong;
+  out[1] = c.nseg;
+  out[2] = c.overflow;
+  out[3] = c.nlist;
+  return 0;
+}
 
 }  // extern "C"

@@ -105,8 +105,8 @@ struct SplitCounters {
   unsigned long long tasks;    // chunk tasks of the span pass (long spans count 1)
   unsigned long long nslices;  // slices of 2^lg_tau tasks
   uint32_t lg_tau;
-  unsigned long long nlist;
-  unsigned long long slice_q, slice_r;  // exact slices: q = T / K, r = T % K    // spans the quad kernel leaves to the generic path
+  unsigned long long nlist;             // spans the quad kernel leaves to the generic path
+  unsigned long long slice_q, slice_r;  // exact slices: q = T / K, r = T % K
 };
 
 struct SplitWs {

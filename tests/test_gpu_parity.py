@@ -24,6 +24,18 @@ def _u32(t):
     return t.cpu().numpy().view(np.uint32)
 
 
+def _last_split(native):
+    """{long spans, segments, overflow flag, quad-listed spans} of this thread's
+    last descriptor batch (test hook prismdb_crc32c_last_split)."""
+    import ctypes
+
+    arr = (ctypes.c_uint64 * 4)()
+    native.prismdb_crc32c_last_split.argtypes = [ctypes.c_void_p]
+    native.prismdb_crc32c_last_split.restype = ctypes.c_int
+    assert native.prismdb_crc32c_last_split(arr) == 0
+    return list(arr)
+
+
 def _to_dev(arr, dev):
     import torch
 
@@ -185,7 +197,7 @@ def test_huge_span_split_path(dev, oracle):
     _check_spans(dev, oracle, host, [3, 17, (40 << 20) + 5], [40 << 20, 131073, 4000])
 
 
-def test_max_length_span(dev, oracle):
+def test_max_length_span(dev, oracle, native):
     """The longest span a descriptor holds (len = 2^32 - 1) at an odd offset,
     with an initial value, Mask and VERIFY against its stored trailer, next to
     a short span with a damaged trailer: the split path's 131 072 segments and
@@ -221,9 +233,46 @@ def test_max_length_span(dev, oracle):
     out, mm = crc32c.batch(buf, d_off, d_len, d_init, mask=True, verify=True)
     np.testing.assert_array_equal(_u32(out), want)
     assert mm.cpu().numpy().tolist() == [0, 1]
+    assert _last_split(native)[:3] == [1, 131072, 0]  # one long span, 2^17 segments, no overflow
     out2, _ = crc32c.batch(buf, d_off[:1], d_len[:1], d_init[:1])  # unmasked, no verify
     assert int(_u32(out2)[0]) == int(raw[0])
     del buf, out, mm, out2
+    torch.cuda.empty_cache()
+
+
+def test_segment_workspace_overflow_fallback(dev, oracle, native):
+    """More long spans than the segment workspace lists (kCapLong = 2^18):
+    the planner flags the overflow and the span pass folds every long span
+    itself as a chain of 4 KiB chunks (no segment pass, no combine).  2^18 +
+    64 spans of 128 KiB + 1 B (just above kLongSpan), one per 131 080-B
+    stride with their stored trailers (34 GB), VERIFY with a per-span init,
+    three trailers damaged."""
+    import torch
+    from prismdb_amd import crc32c
+
+    S, L, n = 131080, 131073, (1 << 18) + 64
+    free, _ = torch.cuda.mem_get_info()
+    if free < n * S + (4 << 30):
+        pytest.skip("not enough device memory for the overflow case")
+    blk = oracle.synth(S, 0x5EED0032)
+    init = 0x2468ACE1
+    want = oracle.mask(int(oracle.batch(blk, [0], [L], [init])[0][0]))
+    blk[L:L + 4] = np.frombuffer(np.uint32(want).tobytes(), dtype=np.uint8)
+    buf = torch.empty(n * S, dtype=torch.uint8, device=dev)
+    buf.view(n, S).copy_(torch.from_numpy(blk).to(dev).expand(n, S))
+    damaged = [0, 777, n - 1]
+    for k in damaged:
+        buf[k * S + L + 2] ^= 0x40
+    d_off = torch.arange(n, dtype=torch.int64, device=dev) * S
+    d_len = torch.full((n,), L, dtype=torch.int32, device=dev)
+    d_init = torch.full((n,), init - (1 << 32) if init >= 1 << 31 else init, dtype=torch.int32, device=dev)
+    out, mm = crc32c.batch(buf, d_off, d_len, d_init, mask=True, verify=True)
+    assert _last_split(native)[2] == 1  # the workspace overflowed: the fallback ran
+    got = _u32(out)
+    assert (got == want).all(), np.flatnonzero(got != want)[:10]
+    m = mm.cpu().numpy()
+    assert np.flatnonzero(m).tolist() == damaged
+    del buf, d_off, d_len, d_init, out, mm
     torch.cuda.empty_cache()
 
 
