@@ -68,6 +68,9 @@
 #ifndef PRISMDB_FIXED_DUMMY_VALU  // measurement knob: ... and this many extra VALU per span pair
 #define PRISMDB_FIXED_DUMMY_VALU 0
 #endif
+#ifndef PRISMDB_SPAN_NOEDGE  // measurement knob: span kernel issues no edge-byte load (wrong with tails / verify)
+#define PRISMDB_SPAN_NOEDGE 0
+#endif
 #ifndef PRISMDB_SPAN_WG_EXIT  // span kernel: groups without a stream leave before the table load
 #define PRISMDB_SPAN_WG_EXIT 1
 #endif
@@ -675,7 +678,13 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
     if (last && lane >= 3u && lane < 3u + tl)
       eoff = hwin ? sat((uint64_t)kLogCrcBack + h + t.r.z + (lane - 3u)) : lane - 3u;
     if (kVerify && last && lane >= 6u && lane < 10u) eoff = (hwin ? 0u : tl) + (lane - 6u);
+#if PRISMDB_SPAN_NOEDGE
+    (void)re;
+    (void)eoff;
+    e = 0u;
+#else
     e = buf_ubyte(re, eoff);
+#endif
   };
 
   // Per-stream chain state.
@@ -821,7 +830,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
     issue(tk[sl][0], wb[sl][0], eb[sl][0]);
     issue(tk[sl][1], wb[sl][1], eb[sl][1]);
   }
-  constexpr int kYounger = 2 * (kR + 1);  // the other slot's two tasks
+  constexpr int kYounger = 2 * (kR + (PRISMDB_SPAN_NOEDGE ? 0 : 1));  // the other slot's two tasks
   for (;;) {
 #pragma unroll
     for (int sl = 0; sl < 2; ++sl) {

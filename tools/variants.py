@@ -54,6 +54,8 @@ VARIANTS = {
     "salu200": {"PRISMDB_FIXED_DUMMY_SALU": 200},
     # span kernel: every group loads the tables, streams or not (as in round 1)
     "no_wg_exit": {"PRISMDB_SPAN_WG_EXIT": 0},
+    # measurement-only: span kernel without its edge-byte load (desc4k stays exact: no tails)
+    "noedge": {"PRISMDB_SPAN_NOEDGE": 1, "PRISMDB_MEASURE_ONLY": 1},
     # planner: a long span's thread writes its segment records alone (as in round 1)
     "plan_serial": {"PRISMDB_PLAN_SERIAL_SEG": 1},
     "valu64": {"PRISMDB_FIXED_DUMMY_VALU": 64},
