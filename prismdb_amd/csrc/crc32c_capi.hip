@@ -370,6 +370,13 @@ int RunBatch(DeviceCtx& ctx, const SpanBatch& base_args, bool desc, bool verify,
     a.slice_start = ws.slice_start;
     a.nslices_dev = &ws.counters->nslices;
   }
+  // Large batches of one-task records take the pair-run kernel (its two
+  // streams read adjacent spans); it is launched next to the general one,
+  // and the one whose schedule the scan did not pick leaves at once.
+  a.pair_kernel = PRISMDB_SPAN_PAIR_RUNS && a.slice_start != nullptr && a.n >= prismdb::dev::kPairMinSpans &&
+                          !(a.flags & prismdb::dev::kFlagLogHeader)
+                      ? 1u
+                      : 0u;
   e = prismdb::dev::launch_span(a, verify, ctx.cus, s);
   if (e != hipSuccess) return FailHip(e, "span kernel launch");
   SpanBatch seg{};

@@ -96,7 +96,16 @@ struct SpanBatch {
   // over the list of spans too long for it; n_dev holds the list length)
   const uint32_t* idx;
   const uint8_t* qrun;  // quad kernel: runs it owns a span of (crc32c_long_list_kernel)
+  // Span role: the pair-run span kernel is launched too (it takes the batch
+  // when the scan finds every record one task; the general kernel then leaves).
+  uint32_t pair_kernel;
 };
+
+#ifndef PRISMDB_SPAN_PAIR_RUNS  // launch the pair-run span kernel for batches of >= kPairMinSpans spans
+#define PRISMDB_SPAN_PAIR_RUNS 1
+#endif
+// Below this many spans the pair-run kernel's extra launch (~5 us) is not worth it.
+constexpr uint64_t kPairMinSpans = 1ull << 16;
 
 struct SplitCounters {
   unsigned long long nseg;

@@ -68,6 +68,9 @@
 #ifndef PRISMDB_FIXED_DUMMY_VALU  // measurement knob: ... and this many extra VALU per span pair
 #define PRISMDB_FIXED_DUMMY_VALU 0
 #endif
+#ifndef PRISMDB_FIXED_FAR_PAIR  // measurement knob: fixed kernel pairs spans half a run apart (the span kernel's pattern)
+#define PRISMDB_FIXED_FAR_PAIR 0
+#endif
 #ifndef PRISMDB_SPAN_NOEDGE  // measurement knob: span kernel issues no edge-byte load (wrong with tails / verify)
 #define PRISMDB_SPAN_NOEDGE 0
 #endif
@@ -103,9 +106,6 @@
 #endif
 #ifndef PRISMDB_SLICE_EXACT  // task-balanced slices: exactly m per stream (1) or ceil(T / 2^lg) (0)
 #define PRISMDB_SLICE_EXACT 1
-#endif
-#ifndef PRISMDB_RUNS_EXACT  // span kernel runs: exactly m per stream (1) or runs of 2^lg records (0)
-#define PRISMDB_RUNS_EXACT 1
 #endif
 #ifndef PRISMDB_RUNS_PER_STREAM  // span kernel: runs of one-task records shrink until every stream gets this many
 #define PRISMDB_RUNS_PER_STREAM 64
@@ -473,7 +473,7 @@ struct Task {
 // and lets invalid or skipped tasks run through the same code.  Records come
 // through the scalar cache, one span ahead per stream.
 // ---------------------------------------------------------------------------
-template <bool kVerify, bool kSkip>
+template <bool kVerify, bool kSkip, bool kPairs>
 __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
   // Chunk geometry: 4 KiB chunks of 16 rounds; kRoundsLog for the log-record
   // kernel (crc32c_device.h).
@@ -519,12 +519,41 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
   const uint32_t S = 2 * nwaves;
   bool sliced = a.slice_start != nullptr;
   uint32_t K = sliced ? (uint32_t)const_load(a.nslices_dev, 0) : 0u;  // <= n/2 + 32 S + 2; 0: runs
-#if PRISMDB_RUNS_EXACT
+  // Pair runs: the scan found every record one task (nslices = 0), so the
+  // wave's two streams advance one record per fold together.  Then they share
+  // the wave's runs and take alternate records (stream st: lo + st, lo + st +
+  // 2, ...), so a fold reads two adjacent spans, as the fixed kernel's pairs
+  // do: streams a run apart (128 KiB) cost the fixed kernel 3.7 %
+  // (profiles/r02af_variants_fixed_far_pair.json).  Runs are counted in
+  // pairs of records (pq or pq+1 pairs, <= 32, exactly m per wave), so only
+  // the batch's last run can be odd, and a run is stored once, when stream
+  // 0's last record of it is folded (stream 1's last is in the same fold, or
+  // the fold before in an odd last run).
+  // The host launches the pair-run kernel (kPairs) next to the general one
+  // for large batches (a.pair_kernel); each leaves if the scan's result is
+  // the other's.  As one kernel with a runtime switch, the two paths' scalar
+  // state spilled SGPRs to scratch.
+  constexpr bool pairs = kPairs;
+  const bool pair_batch = sliced && K == 0;
+  if (kPairs ? !pair_batch : (pair_batch && a.pair_kernel != 0u)) return;
   // Runs: K = m S runs of q or q+1 records (q <= 63, runs 0..r-1 the longer),
   // exactly m per stream; m >= PRISMDB_RUNS_PER_STREAM while runs keep >= 1
   // record.  (Runs of 2^lg records left a stream the ceil or floor of K/S.)
   uint32_t rq = 0, rr = 0;
-  if (K == 0) {
+  if (pairs) {
+    sliced = false;
+    const uint32_t np = (n + 1u) / 2u;  // pairs of records
+    const uint32_t rps = (uint32_t)PRISMDB_RUNS_PER_STREAM;
+    uint32_t m = (uint32_t)(((uint64_t)np + 31ull * nwaves - 1u) / (31ull * nwaves));  // <= 32 pairs a run
+    if (m < rps) {
+      const uint32_t mr = np / nwaves;
+      m = mr < rps ? (mr > m ? mr : m) : rps;
+    }
+    if (m < 1u) m = 1u;
+    K = (uint64_t)m * nwaves < np ? m * nwaves : np;
+    rq = np / K;
+    rr = np % K;
+  } else if (K == 0) {
     sliced = false;
     const uint32_t rps = (uint32_t)PRISMDB_RUNS_PER_STREAM;
     uint32_t m = (uint32_t)(((uint64_t)n + 63ull * S - 1u) / (63ull * S));
@@ -537,20 +566,15 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
     rq = n / K;
     rr = n % K;
   }
-#else
-  uint32_t lg = 6;
-  if (K == 0) {
-    sliced = false;
-    while (lg > 0 && (n >> (lg + 1)) < nwaves * (uint32_t)PRISMDB_RUNS_PER_STREAM) --lg;
-    K = (uint32_t)(((uint64_t)n + (1u << lg) - 1) >> lg);
-  }
-#endif
   // A group whose streams (2 per wave) are all >= K has no slice or run: it
   // leaves before loading the tables (the segment pass of a batch with a few
   // long spans launches the whole grid for a handful of streams).
-  if (PRISMDB_SPAN_WG_EXIT && blockIdx.x * 2u * kWavesPerGroup >= K) return;
+  if (PRISMDB_SPAN_WG_EXIT && blockIdx.x * (pairs ? 1u : 2u) * kWavesPerGroup >= K) return;
+
 
   __shared__ uint32_t lds[kLdsWords];
+  const uint32_t kstep = pairs ? nwaves : S;  // a stream's next run: k + kstep
+  constexpr uint32_t bstep = pairs ? 2u : 1u;  // its next record in a run: b + bstep
   load_tables(lds, a.tabs, tid);
   __syncthreads();
   const StrideLanes tab = stride_lanes(lane);
@@ -561,24 +585,26 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
   struct Cursor {
     uint32_t b, lo, hi, k;
   };
-  auto open = [&](Cursor& c, uint32_t k) {  // first non-empty slice >= k of the stream
-    for (; k < K; k += S) {
+  // first slice or run >= k of stream st with a record for it
+  auto open = [&](Cursor& c, uint32_t k, uint32_t st) {
+    for (; k < K; k += kstep) {
       uint32_t lo, hi;
       if (sliced) {
         lo = (uint32_t)const_load(a.slice_start, k);
         hi = (uint32_t)const_load(a.slice_start, k + 1);
       } else {
-#if PRISMDB_RUNS_EXACT
         lo = k * rq + (k < rr ? k : rr);
         hi = lo + rq + (k < rr ? 1u : 0u);
-#else
-        lo = k << lg;
-        hi = (uint32_t)((uint64_t)lo + (1u << lg) < n ? lo + (1u << lg) : n);
-#endif
+        if (pairs) {  // runs of pairs: records [2 lo, 2 hi)
+          lo *= 2u;
+          hi *= 2u;
+        }
       }
       hi = hi < n ? hi : n;
-      if (lo < hi) {
-        c.b = c.lo = lo;
+      const uint32_t b = lo + (pairs ? st : 0u);
+      if (b < hi) {
+        c.b = b;
+        c.lo = lo;
         c.hi = hi;
         c.k = k;
         return;
@@ -587,9 +613,9 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
     c.b = c.lo = c.hi = n;
     c.k = K;
   };
-  auto advance = [&](Cursor& c) {
-    if (c.b + 1 < c.hi) ++c.b;
-    else open(c, c.k + S);
+  auto advance = [&](Cursor& c, uint32_t st) {
+    if (c.b + bstep < c.hi) c.b += bstep;
+    else open(c, c.k + kstep, st);
   };
 
   auto read_rec = [&](uint32_t b) -> SpanRec {
@@ -604,7 +630,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
     t.c = 0;
     const bool valid = c.b < n;
     const bool skip = !valid || (skip_long && t.lng());
-    t.f = (c.b - c.lo) | (c.b + 1 == c.hi ? 1u << 8 : 0u) | (valid ? 1u << 9 : 0u) | (skip ? 1u << 10 : 0u);
+    t.f = (c.b - c.lo) | (c.b + bstep >= c.hi ? 1u << 8 : 0u) | (valid ? 1u << 9 : 0u) | (skip ? 1u << 10 : 0u);
     return t;
   };
   Cursor cur[2];
@@ -625,7 +651,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
     for (int s = 0; s < 2; ++s) {
       if (refill[s]) {
         refill[s] = false;
-        advance(cur[s]);
+        advance(cur[s], (uint32_t)s);
         pend[s] = read_rec(cur[s].b);
       }
     }
@@ -734,6 +760,19 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
       if (kVerify && a.mismatch != nullptr) __builtin_nontemporal_store((uint8_t)bad[s], a.mismatch + base + lane);
     }
   };
+  // Pair runs: the run ending with stream 0's task t, lanes [0, t.slot() + 1]
+  // (those below n), even lanes from stream 0, odd lanes from stream 1.
+  auto flush_pair = [&](const Task& t) {
+    const uint32_t base = t.b - t.slot();
+    if (lane <= t.slot() + 1u && base + lane < n) {
+      // by masks, not `odd ? res[1] : res[0]`: hipcc folds that select into
+      // res[odd], an indexed array, and moves res and bad to scratch
+      const uint32_t odd = 0u - (lane & 1u);
+      if (a.out != nullptr) __builtin_nontemporal_store(res[0] ^ ((res[0] ^ res[1]) & odd), a.out + base + lane);
+      if (kVerify && a.mismatch != nullptr)
+        __builtin_nontemporal_store((uint8_t)(bad[0] ^ ((bad[0] ^ bad[1]) & odd)), a.mismatch + base + lane);
+    }
+  };
   // End of a span: tail bytes, conditioning, outputs.
   auto finish = [&](int s, const Task& t, uint32_t e, uint32_t body) {
     const uint32_t tl = t.t();
@@ -748,7 +787,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
     }
     if ((a.flags & kFlagWriteTrailer) && lane == 0)
       store_le32(hdr ? t.start() - kLogCrcBack : t.body() + t.r.z + tl, v);
-    if (t.last()) flush(s, t);
+    if (!pairs && t.last()) flush(s, t);
   };
   // Fold the pair (stream 0 task tx in wx, stream 1 task ty in wy).
   auto fold = [&](const Task& tx, uint32_t (&wx)[kR], uint32_t ex, const Task& ty,
@@ -801,10 +840,15 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
     } else if (endy) {
       finish(1, ty, ey, wave_xor(realign(lds, nibtab, ay)));
     }
-    // A skipped long span's result comes from the combine pass, but it may
-    // close its slice: the slice's other results are stored now.
-    if (tx.skip() && tx.valid() && tx.last()) flush(0, tx);
-    if (ty.skip() && ty.valid() && ty.last()) flush(1, ty);
+    if (pairs) {
+      // the run is complete once stream 0's last record of it is folded
+      if (tx.valid() && tx.last()) flush_pair(tx);
+    } else {
+      // A skipped long span's result comes from the combine pass, but it may
+      // close its slice: the slice's other results are stored now.
+      if (tx.skip() && tx.valid() && tx.last()) flush(0, tx);
+      if (ty.skip() && ty.valid() && ty.last()) flush(1, ty);
+    }
   };
 
   // Ring: two slots x two streams, compile-time slot indices (loop unrolled
@@ -816,9 +860,9 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
   uint32_t eb[2][2];
 #pragma unroll
   for (int st = 0; st < 2; ++st) {
-    open(cur[st], 2 * wave + st);
+    open(cur[st], pairs ? wave : 2 * wave + st, (uint32_t)st);
     tk[0][st] = make_task(cur[st], read_rec(cur[st].b));
-    advance(cur[st]);
+    advance(cur[st], (uint32_t)st);
     pend[st] = read_rec(cur[st].b);
   }
   if (!tk[0][0].valid() && !tk[0][1].valid()) return;
@@ -893,8 +937,16 @@ __global__ __launch_bounds__(kThreads) void crc32c_fixed_kernel(SpanBatch a) {
   const uint64_t kRun = 2ull << lg;
   // First span of the wave's next pair step: +2 inside a run, then on to the
   // wave's next run (the other waves' runs in between).
+#if PRISMDB_FIXED_FAR_PAIR
+  // pair = spans (r0 + i, r0 + kRun/2 + i): two sequential streams half a run apart
+  const uint64_t kHalf = kRun / 2u, kSecond = kHalf;
+  const uint64_t jump = (nwaves - 1u) * kRun + kHalf + 1u;
+  auto adv = [&](uint64_t x) -> uint64_t { return ((x + 1u) & (kHalf - 1u)) ? x + 1u : x + jump; };
+#else
+  const uint64_t kSecond = 1u;
   const uint64_t jump = (nwaves - 1u) * kRun + 2u;
   auto adv = [&](uint64_t x) -> uint64_t { return ((x + 2u) & (kRun - 1u)) ? x + 2u : x + jump; };
+#endif
   uint64_t cur = wave * kRun;  // first span of the pair being folded
   if (cur >= n) return;
 
@@ -949,7 +1001,11 @@ __global__ __launch_bounds__(kThreads) void crc32c_fixed_kernel(SpanBatch a) {
     const uint32_t va = realign(lds, nibtab, acc_a), vb = realign(lds, nibtab, acc_b);
 #endif
     const uint32_t ca = wave_xor(va) ^ kConditioning, cb = wave_xor(vb) ^ kConditioning;
-    const uint32_t i = (uint32_t)(cur & (kRun - 1u));  // the pair's lanes in the run
+#if PRISMDB_FIXED_FAR_PAIR
+    const uint32_t i = (uint32_t)(cur & (kHalf - 1u)), i2 = i + (uint32_t)kHalf;  // the pair's lanes in the run
+#else
+    const uint32_t i = (uint32_t)(cur & (kRun - 1u)), i2 = i + 1u;  // the pair's lanes in the run
+#endif
 #if PRISMDB_FIXED_DUMMY_SALU
     {  // sensitivity probe: a dependent chain of scalar ALU work
       uint32_t d = i;
@@ -964,18 +1020,18 @@ __global__ __launch_bounds__(kThreads) void crc32c_fixed_kernel(SpanBatch a) {
     }
 #endif
     res = lane == i ? (masked ? mask_crc(ca) : ca) : res;
-    res = lane == i + 1u ? (masked ? mask_crc(cb) : cb) : res;
+    res = lane == i2 ? (masked ? mask_crc(cb) : cb) : res;
     if (kVerify) {
       const uint32_t ba = ca != unmask_crc(readlane(wa[0], 0)) ? 1u : 0u;
       const uint32_t bb = cb != unmask_crc(readlane(wb[0], 0)) ? 1u : 0u;
       bad = lane == i ? ba : bad;
-      bad = lane == i + 1u ? bb : bad;
+      bad = lane == i2 ? bb : bad;
     }
   };
   // Run end (or the last pair): lanes 0..i+1 hold results of spans b0 + lane.
   auto flush = [&]() {
     const uint64_t b0 = cur & ~(kRun - 1u);
-    const uint32_t last = (uint32_t)(cur & (kRun - 1u)) + 1u;
+    const uint32_t last = PRISMDB_FIXED_FAR_PAIR ? (uint32_t)kRun - 1u : (uint32_t)(cur & (kRun - 1u)) + 1u;
     // nt: the results are not re-read; a streaming store keeps them from
     // contending with the read stream (0.6 % of the read rate vs 2 %, probes).
     if (!PRISMDB_FIXED_NOSTORE && lane <= last && b0 + lane < n) {
@@ -994,7 +1050,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_fixed_kernel(SpanBatch a) {
 #pragma unroll
   for (int d = 0; d < kRing; d += 2) {
     issue(ahead, ring[d]);
-    issue(ahead + 1, ring[d + 1]);
+    issue(ahead + kSecond, ring[d + 1]);
     ahead = adv(ahead);
   }
   // One exit, at the bottom of a whole ring turn: steps past the wave's last
@@ -1013,7 +1069,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_fixed_kernel(SpanBatch a) {
       }
       cur = nxt;
       issue(ahead, ring[s]);
-      issue(ahead + 1, ring[s + 1]);
+      issue(ahead + kSecond, ring[s + 1]);
       ahead = adv(ahead);
     }
     if (cur >= n) break;
@@ -1876,11 +1932,13 @@ hipError_t launch_span(const SpanBatch& a, bool verify, int grid, hipStream_t s)
   // Log records (LOG_HEADER) are short: the variant that skips padding rounds.
   const bool skip = (a.flags & kFlagLogHeader) != 0 && a.role == kRoleSpans;
   if (verify) {
-    if (skip) crc32c_span_kernel<true, true><<<grid, kThreads, 0, s>>>(a);
-    else crc32c_span_kernel<true, false><<<grid, kThreads, 0, s>>>(a);
+    if (a.pair_kernel && !skip) crc32c_span_kernel<true, false, true><<<grid, kThreads, 0, s>>>(a);
+    if (skip) crc32c_span_kernel<true, true, false><<<grid, kThreads, 0, s>>>(a);
+    else crc32c_span_kernel<true, false, false><<<grid, kThreads, 0, s>>>(a);
   } else {
-    if (skip) crc32c_span_kernel<false, true><<<grid, kThreads, 0, s>>>(a);
-    else crc32c_span_kernel<false, false><<<grid, kThreads, 0, s>>>(a);
+    if (a.pair_kernel && !skip) crc32c_span_kernel<false, false, true><<<grid, kThreads, 0, s>>>(a);
+    if (skip) crc32c_span_kernel<false, true, false><<<grid, kThreads, 0, s>>>(a);
+    else crc32c_span_kernel<false, false, false><<<grid, kThreads, 0, s>>>(a);
   }
   return hipGetLastError();
 }

@@ -197,6 +197,41 @@ def test_huge_span_split_path(dev, oracle):
     _check_spans(dev, oracle, host, [3, 17, (40 << 20) + 5], [40 << 20, 131073, 4000])
 
 
+@pytest.mark.parametrize("n", [65536, 65537, 200001])
+def test_pair_run_schedule(dev, oracle, native, n):
+    """Batches the pair-run span kernel takes (>= 2^16 spans, every span one
+    task): random lengths 0..4096 at random offsets, one in 997 a long span
+    (split path) instead, per-span init, Mask, VERIFY with every seventh
+    trailer damaged; odd counts leave an odd last run."""
+    import torch
+    from prismdb_amd import crc32c
+
+    rng = np.random.default_rng(0x5EED0040 + n)
+    lens = rng.integers(0, 4097, size=n).astype(np.int64)
+    lens[::997] = rng.integers(131073, 400000, size=len(lens[::997]))
+    slots = lens + 4
+    off = np.concatenate([[11], 11 + np.cumsum(slots + rng.integers(0, 9, size=n))[:-1]]).astype(np.uint64)
+    size = int(off[-1] + lens[-1] + 4 + 8)
+    host = oracle.synth(size, 0x5EED0041)
+    init = rng.integers(0, 2**32, size=n, dtype=np.uint64).astype(np.uint32)
+    raw, _ = oracle.batch(host, off, lens.astype(np.uint32), init)
+    masked = np.array([oracle.mask(int(c)) for c in raw], dtype=np.uint32)
+    damaged = np.zeros(n, dtype=bool)
+    damaged[3::7] = True
+    stored = masked ^ damaged.astype(np.uint32)
+    tr = (off + lens.astype(np.uint64)).astype(np.int64)[:, None] + np.arange(4)[None, :]
+    host[tr] = stored.astype("<u4").view(np.uint8).reshape(-1, 4)
+    buf = torch.from_numpy(host).to(dev)
+    d_off = torch.from_numpy(off.astype(np.int64)).to(dev)
+    d_len = torch.from_numpy(lens.astype(np.uint32).view(np.int32)).to(dev)
+    d_init = torch.from_numpy(init.view(np.int32)).to(dev)
+    out, mm = crc32c.batch(buf, d_off, d_len, d_init, mask=True, verify=True)
+    np.testing.assert_array_equal(_u32(out), masked)
+    np.testing.assert_array_equal(mm.cpu().numpy(), damaged.astype(np.uint8))
+    out2, _ = crc32c.batch(buf, d_off, d_len)  # no init / mask / verify
+    np.testing.assert_array_equal(_u32(out2), oracle.batch(host, off, lens.astype(np.uint32))[0])
+
+
 def test_max_length_span(dev, oracle, native):
     """The longest span a descriptor holds (len = 2^32 - 1) at an odd offset,
     with an initial value, Mask and VERIFY against its stored trailer, next to

@@ -56,6 +56,10 @@ VARIANTS = {
     "no_wg_exit": {"PRISMDB_SPAN_WG_EXIT": 0},
     # measurement-only: span kernel without its edge-byte load (desc4k stays exact: no tails)
     "noedge": {"PRISMDB_SPAN_NOEDGE": 1, "PRISMDB_MEASURE_ONLY": 1},
+    # measurement: fixed kernel pairs spans half a run apart, like the span kernel's two streams
+    "far_pair": {"PRISMDB_FIXED_FAR_PAIR": 1},
+    # span kernel: streams in their own runs even when every record is one task (round 1)
+    "no_pair_runs": {"PRISMDB_SPAN_PAIR_RUNS": 0},
     # planner: a long span's thread writes its segment records alone (as in round 1)
     "plan_serial": {"PRISMDB_PLAN_SERIAL_SEG": 1},
     "valu64": {"PRISMDB_FIXED_DUMMY_VALU": 64},
