@@ -104,8 +104,9 @@ struct SpanBatch {
 #ifndef PRISMDB_SPAN_PAIR_RUNS  // launch the pair-run span kernel for batches of >= kPairMinSpans spans
 #define PRISMDB_SPAN_PAIR_RUNS 1
 #endif
-// Below this many spans the pair-run kernel's extra launch (~5 us) is not worth it.
-constexpr uint64_t kPairMinSpans = 1ull << 16;
+// Below this many spans the pair-run kernel's extra launch (~5 us) costs more
+// than its 3.5 % gains (break-even near 140 us of data, ~250 K spans of 4 KiB).
+constexpr uint64_t kPairMinSpans = 1ull << 18;
 
 struct SplitCounters {
   unsigned long long nseg;

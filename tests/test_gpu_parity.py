@@ -197,9 +197,9 @@ def test_huge_span_split_path(dev, oracle):
     _check_spans(dev, oracle, host, [3, 17, (40 << 20) + 5], [40 << 20, 131073, 4000])
 
 
-@pytest.mark.parametrize("n", [65536, 65537, 200001])
+@pytest.mark.parametrize("n", [1 << 18, (1 << 18) + 1, 300001])
 def test_pair_run_schedule(dev, oracle, native, n):
-    """Batches the pair-run span kernel takes (>= 2^16 spans, every span one
+    """Batches the pair-run span kernel takes (>= 2^18 spans, every span one
     task): random lengths 0..4096 at random offsets, one in 997 a long span
     (split path) instead, per-span init, Mask, VERIFY with every seventh
     trailer damaged; odd counts leave an odd last run."""
