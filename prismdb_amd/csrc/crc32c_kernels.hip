@@ -534,7 +534,9 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
   // the other's.  As one kernel with a runtime switch, the two paths' scalar
   // state spilled SGPRs to scratch.
   constexpr bool pairs = kPairs;
-  const bool pair_batch = sliced && K == 0;
+  // (not after a segment-workspace overflow: long spans are then folded here
+  // as chains of chunks, but the scan counted them one task each)
+  const bool pair_batch = sliced && K == 0 && skip_long;
   if (kPairs ? !pair_batch : (pair_batch && a.pair_kernel != 0u)) return;
   // Runs: K = m S runs of q or q+1 records (q <= 63, runs 0..r-1 the longer),
   // exactly m per stream; m >= PRISMDB_RUNS_PER_STREAM while runs keep >= 1

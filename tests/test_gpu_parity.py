@@ -281,30 +281,35 @@ def test_segment_workspace_overflow_fallback(dev, oracle, native):
     itself as a chain of 4 KiB chunks (no segment pass, no combine).  2^18 +
     64 spans of 128 KiB + 1 B (just above kLongSpan), one per 131 080-B
     stride with their stored trailers (34 GB), VERIFY with a per-span init,
-    three trailers damaged."""
+    three trailers damaged.  Every other span is 65 536 B longer (49 chunks
+    against 33): the fallback chains then have different lengths, which the
+    pair-run schedule (one task per record) must not take."""
     import torch
     from prismdb_amd import crc32c
 
-    S, L, n = 131080, 131073, (1 << 18) + 64
+    S, L, L2, n = 196624, 131073, 196609, (1 << 18) + 64
     free, _ = torch.cuda.mem_get_info()
     if free < n * S + (4 << 30):
         pytest.skip("not enough device memory for the overflow case")
-    blk = oracle.synth(S, 0x5EED0032)
+    pat = oracle.synth(2 * S, 0x5EED0032)  # two stride blocks, repeated
     init = 0x2468ACE1
-    want = oracle.mask(int(oracle.batch(blk, [0], [L], [init])[0][0]))
-    blk[L:L + 4] = np.frombuffer(np.uint32(want).tobytes(), dtype=np.uint8)
+    want = [oracle.mask(int(c)) for c in oracle.batch(pat, [0, S], [L, L2], [init, init])[0]]
+    pat[L:L + 4] = np.frombuffer(np.uint32(want[0]).tobytes(), dtype=np.uint8)
+    pat[S + L2:S + L2 + 4] = np.frombuffer(np.uint32(want[1]).tobytes(), dtype=np.uint8)
     buf = torch.empty(n * S, dtype=torch.uint8, device=dev)
-    buf.view(n, S).copy_(torch.from_numpy(blk).to(dev).expand(n, S))
+    buf.view(n // 2, 2 * S).copy_(torch.from_numpy(pat).to(dev).expand(n // 2, 2 * S))
+    lens = np.where(np.arange(n) % 2 == 0, L, L2)
     damaged = [0, 777, n - 1]
     for k in damaged:
-        buf[k * S + L + 2] ^= 0x40
+        buf[k * S + int(lens[k]) + 2] ^= 0x40
     d_off = torch.arange(n, dtype=torch.int64, device=dev) * S
-    d_len = torch.full((n,), L, dtype=torch.int32, device=dev)
+    d_len = torch.from_numpy(lens.astype(np.int32)).to(dev)
     d_init = torch.full((n,), init - (1 << 32) if init >= 1 << 31 else init, dtype=torch.int32, device=dev)
     out, mm = crc32c.batch(buf, d_off, d_len, d_init, mask=True, verify=True)
     assert _last_split(native)[2] == 1  # the workspace overflowed: the fallback ran
     got = _u32(out)
-    assert (got == want).all(), np.flatnonzero(got != want)[:10]
+    wantv = np.where(np.arange(n) % 2 == 0, want[0], want[1]).astype(np.uint32)
+    assert (got == wantv).all(), np.flatnonzero(got != wantv)[:10]
     m = mm.cpu().numpy()
     assert np.flatnonzero(m).tolist() == damaged
     del buf, d_off, d_len, d_init, out, mm
