@@ -68,6 +68,9 @@
 #ifndef PRISMDB_FIXED_DUMMY_VALU  // measurement knob: ... and this many extra VALU per span pair
 #define PRISMDB_FIXED_DUMMY_VALU 0
 #endif
+#ifndef PRISMDB_QUAD_UNALIGNED  // quad kernel: body words from the record's first byte (unaligned dword loads, no head bytes)
+#define PRISMDB_QUAD_UNALIGNED 0
+#endif
 #ifndef PRISMDB_FIXED_FAR_PAIR  // measurement knob: fixed kernel pairs spans half a run apart (the span kernel's pattern)
 #define PRISMDB_FIXED_FAR_PAIR 0
 #endif
@@ -1663,8 +1666,9 @@ __global__ __launch_bounds__(kThreads) void crc32c_quad_kernel(SpanBatch a) {
     const uint32_t ln = sel(len[0], len[1], len[2], len[3]);
     const bool ok = (win.mask >> g) & 1u;
     vpo = ok ? base_sb + sel((uint32_t)off[0], (uint32_t)off[1], (uint32_t)off[2], (uint32_t)off[3]) : 8u;
-    // head bytes up to 4-B alignment of the absolute address
-    uint32_t h = (0u - ((uint32_t)win.sb + vpo)) & 3u;
+    // head bytes up to 4-B alignment of the absolute address (none with
+    // unaligned body loads: the body starts at the record's first byte)
+    uint32_t h = PRISMDB_QUAD_UNALIGNED ? 0u : (0u - ((uint32_t)win.sb + vpo)) & 3u;
     h = h < ln ? h : ln;
     uint32_t W = (ln - h) >> 2, t = (ln - h) & 3u;
     if (!ok) W = h = t = 0u;
