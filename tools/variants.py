@@ -48,6 +48,8 @@ VARIANTS = {
     "quad_clamped": {"PRISMDB_QUAD_CLAMPED": 1},
     # quad kernel: unaligned body loads from the record's first byte (no head product)
     "quad_unaligned": {"PRISMDB_QUAD_UNALIGNED": 1},
+    # (A/B helper: built from an older kernel source copied into the tree)
+    "older_src": {"PRISMDB_OLDER_SRC": 1},
     # span kernel: initial register folded in (no ring-register copies at the merge)
     "inj_fold": {"PRISMDB_SPAN_INJ_RING": 0},
     # measurement-only: span kernel waits for every record's scalar read right away
