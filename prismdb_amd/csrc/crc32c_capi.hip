@@ -72,6 +72,7 @@ int g_quad_mode = PRISMDB_QUAD_DEFAULT;
 void BuildTables(DeviceTables* t) {
   namespace g = prismdb::gf2;
   g::StrideTables(prismdb::dev::kStrideBytes, t->stride);
+  g::StrideTables(4u, t->slice4);
   for (int l = 0; l < 64; ++l) {
     const g::Op m = g::ShiftBytes(prismdb::dev::kStrideBytes - 4u * (uint32_t)l);
     for (int n = 0; n < 8; ++n)

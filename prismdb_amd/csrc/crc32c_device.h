@@ -46,6 +46,7 @@ struct DeviceTables {
   uint32_t shift_seg[32];     // column i of shift_kSegment (M)
   uint32_t shift_seg64[32];   // column i of M^64
   uint32_t lane_seg[32][64];  // [i][l] = column i of M^(63-l): lane l's final shift
+  uint32_t slice4[4][256];    // slice4[k][b] = shift_4(b << 8k): one record per lane (lane kernel)
   // 64 KiB of zeros: the quad kernel's loads of lanes without a record to
   // read land here, 256 B per wave (wave % 256) -- one shared line was an L2
   // hotspot when whole tasks are left to the generic path
@@ -61,6 +62,19 @@ constexpr uint32_t kQuadMaxLen = 4u * kQuadWords;    // len <= 1280 B => <= 320 
 // A record's body-address arithmetic reaches kQuadBack bytes below its body
 // (unsigned, 32-bit offsets from the task's window base).
 constexpr uint32_t kQuadBack = kQuadMaxLen;
+
+// Lane kernel (log-record batches): one record per lane, 128-B tasks of eight
+// 16-B loads; records of kLaneMinLen..kLaneMaxLen bytes (the rest take the
+// generic path through the long-span list, as with the quad kernel).
+#ifndef PRISMDB_LANE_KERNEL
+#define PRISMDB_LANE_KERNEL 1
+#endif
+constexpr uint32_t kLaneMinLen = 20u;   // >= 3 head bytes + one 16-B body chunk + the 16-B tail load
+constexpr uint32_t kLaneMaxLen = 1280u;
+// off >= 3: the head dword (4-B aligned, at or below the record) stays in the buffer
+__host__ __device__ constexpr bool lane_owns(uint32_t len, uint64_t off) {
+  return len >= kLaneMinLen && len <= kLaneMaxLen && off >= 3u;
+}
 
 enum : uint32_t { kRoleSpans = 0, kRoleSegments = 1 };
 
@@ -140,6 +154,7 @@ struct SplitWs {
   uint32_t* qout;         // quad path: generic-path results of the listed spans (list order)
   uint8_t* qmm;
   uint8_t* qrun;          // quad path: per run of 64 spans, 1 if the quad kernel owns one of them
+                          // (read a dword at a time: the workspace has slack around it)
 };
 
 constexpr uint32_t kMaxPlanBlocks = 4096;

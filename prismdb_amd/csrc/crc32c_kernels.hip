@@ -74,6 +74,15 @@
 #ifndef PRISMDB_FIXED_FAR_PAIR  // measurement knob: fixed kernel pairs spans half a run apart (the span kernel's pattern)
 #define PRISMDB_FIXED_FAR_PAIR 0
 #endif
+#ifndef PRISMDB_FIXED_CHAIN  // measurement knob: the pair's second span starts from the first's register (one dependent chain; wrong results)
+#define PRISMDB_FIXED_CHAIN 0
+#endif
+#ifndef PRISMDB_LANE_NOFOLD  // measurement knob: lane kernel XORs its words instead of folding them (wrong results)
+#define PRISMDB_LANE_NOFOLD 0
+#endif
+#ifndef PRISMDB_LANE_ALIGNED  // measurement knob: lane kernel body load addresses & ~this (15: 16-B aligned; wrong results)
+#define PRISMDB_LANE_ALIGNED 0
+#endif
 #ifndef PRISMDB_SPAN_NOEDGE  // measurement knob: span kernel issues no edge-byte load (wrong with tails / verify)
 #define PRISMDB_SPAN_NOEDGE 0
 #endif
@@ -344,6 +353,16 @@ template <typename T>
 __device__ __forceinline__ T const_load(const T* p, uint64_t i) {
   typedef const __attribute__((address_space(4))) T CT;
   return ((CT*)p)[i];
+}
+
+// A byte through the scalar cache: the aligned dword holding it (s_load has
+// no byte form; a plain byte read compiles to a vector load and a vmcnt(0)
+// that drains the kernels' load rings).  The dword may reach 3 bytes before
+// or after the array: callers' arrays have slack on both sides.
+__device__ __forceinline__ uint32_t const_byte(const uint8_t* p, uint64_t i) {
+  const uint64_t ad = reinterpret_cast<uint64_t>(p) + i;
+  const uint32_t w = const_load(reinterpret_cast<const uint32_t*>(ad & ~3ull), 0);
+  return (w >> (8u * (uint32_t)(ad & 3u))) & 255u;
 }
 
 __device__ __forceinline__ u32x4 buffer_rsrc(const uint8_t* p, uint32_t bytes) {
@@ -998,11 +1017,19 @@ __global__ __launch_bounds__(kThreads) void crc32c_fixed_kernel(SpanBatch a) {
     }
     const uint32_t va = acc_a, vb = acc_b;
 #else
+#if PRISMDB_FIXED_CHAIN
+#pragma unroll
+    for (int j = 1; j < K; ++j) acc_a = step256(lds, tab, acc_a, wa[j]);
+    acc_b ^= acc_a;  // the second span continues the first's chain (sequential rounds)
+#pragma unroll
+    for (int j = 1; j < K; ++j) acc_b = step256(lds, tab, acc_b, wb[j]);
+#else
 #pragma unroll
     for (int j = 1; j < K; ++j) {
       acc_a = step256(lds, tab, acc_a, wa[j]);
       acc_b = step256(lds, tab, acc_b, wb[j]);
     }
+#endif
     const uint32_t va = realign(lds, nibtab, acc_a), vb = realign(lds, nibtab, acc_b);
 #endif
     const uint32_t ca = wave_xor(va) ^ kConditioning, cb = wave_xor(vb) ^ kConditioning;
@@ -1604,7 +1631,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_quad_kernel(SpanBatch a) {
   // kernel, read through the scalar cache) are skipped whole.
   const uint8_t* const qrun = a.qrun;
   auto next_run = [&](uint32_t rb) -> uint32_t {  // first owned run at or after rb, its first record
-    while (rb < n && const_load(qrun, (uint64_t)(rb >> 6)) == 0u) rb += 64u * nwaves;
+    while (rb < n && const_byte(qrun, (uint64_t)(rb >> 6)) == 0u) rb += 64u * nwaves;
     return rb;
   };
   auto adv = [&](uint32_t tb) -> uint32_t {
@@ -1869,12 +1896,315 @@ __global__ __launch_bounds__(kThreads) void crc32c_quad_kernel(SpanBatch a) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// Short records, one per lane (crc32c_lane_kernel).  Log records (~1 KB) are
+// too short for a wave-wide fold: the span kernel spends a realignment, a
+// reduction and ~190 scalar instructions on each, the quad kernel (above)
+// still a quarter of that plus masked rounds.  Here lane i of a wave runs the
+// reference's own serial recurrence over record i of a run of 64:
+// r <- shift_4(r ^ word), one word per step, four conflict-free LDS lookups
+// in the slicing tables slice4[k][b] = shift_4(b << 8k) (the same LDS image
+// and v_perm addresses as the stride tables) -- the same lookups per byte as
+// the wave-wide fold, with no realignment, no cross-lane reduction and no
+// per-record scalar work.  A record is h <= 3 head bytes up to 4-B
+// alignment, then 16-B chunks (read with 4-B aligned 16-B loads: byte-
+// unaligned ones measured 16 % slower), then T <= 15 tail bytes.  The head
+// bytes come from the aligned dword holding the record's first byte, the tail
+// from one 16-B load ending at the record's end: its words funnel-shifted out
+// at fixed dword positions from the end, its last T % 4 bytes the top bytes
+// of its last dword.  Bytes go through byte steps (shift_1(y) = y >> 8 ^
+// slice4[3][y & 255]).
+//
+// A task is 128 B of every lane's chunks: eight global_load_dwordx4, issued
+// one task ahead into a two-slot ring and retired by counted vmcnt waits.
+// Tasks before the run's shortest record ends fold unmasked; later ones keep
+// a lane's register past its last word and clamp its loads onto the record's
+// last chunk (every load stays inside the record).
+// Records of kLaneMinLen..kLaneMaxLen bytes are the kernel's (lane_owns);
+// the long-span list sends the rest down the generic path.
+//
+// Load order inside an issue: the next run's descriptors (first task of a
+// run), the run's edge dwords (last task), then the eight body loads, so the
+// body loads of the other slot are always the youngest eight: after a
+// vmcnt(8) wait every descriptor and edge load issued so far has landed.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void load_slice_tables(uint32_t* lds, const DeviceTables* tabs, uint32_t tid) {
+  for (uint32_t w = tid; w < (uint32_t)kTabWords; w += kThreads) {
+    const uint32_t k = ((w >> 14) << 1) | ((w >> 5) & 1u), e = (w >> 6) & 255u;
+    lds[w] = tabs->slice4[k][e];
+  }
+}
+
+__device__ __forceinline__ u32x4 asm_load_x4(uint64_t addr) {
+  u32x4 r;
+  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(r) : "v"(addr));
+  return r;
+}
+template <int kImm>
+__device__ __forceinline__ u32x4 asm_load_x4_at(uint64_t addr) {
+  u32x4 r;
+  asm volatile("global_load_dwordx4 %0, %1, off offset:%2" : "=v"(r) : "v"(addr), "n"(kImm));
+  return r;
+}
+__device__ __forceinline__ uint32_t asm_load_u32(uint64_t addr) {
+  uint32_t r;
+  asm volatile("global_load_dword %0, %1, off" : "=v"(r) : "v"(addr));
+  return r;
+}
+__device__ __forceinline__ uint64_t asm_load_u64(uint64_t addr) {
+  uint64_t r;
+  asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(r) : "v"(addr));
+  return r;
+}
+
+// Wait for a slot's loads (w: body, hd: head dword, ev: the record's last
+// 16 bytes, sc: stored crc) with the other slot's eight body loads in flight;
+// the slot's registers and the prefetched descriptors are in/out operands.
+__device__ __forceinline__ void wait_lane(u32x4 (&w)[8], uint32_t& hd, u32x4& ev, uint32_t& sc, uint64_t& noff,
+                                          uint32_t& nlen, uint32_t& ninit) {
+  asm volatile("s_waitcnt vmcnt(8)"
+               : "+v"(w[0]), "+v"(w[1]), "+v"(w[2]), "+v"(w[3]), "+v"(w[4]), "+v"(w[5]), "+v"(w[6]),
+                 "+v"(w[7]), "+v"(hd), "+v"(ev), "+v"(sc), "+v"(noff), "+v"(nlen), "+v"(ninit)
+               :
+               : "memory");
+}
+
+// Wave-uniform task: run of records [rb, rb + 64), its 128-B task k of K, the
+// first kf unmasked; nrb: the wave's next owned run.
+struct LaneTask {
+  uint32_t rb, k, kf, K, nrb;
+};
+
+template <int kOp>  // 0: max, 1: min
+__device__ __forceinline__ uint32_t wave_reduce(uint32_t v) {
+  auto f = [](uint32_t x, uint32_t y) { return kOp == 0 ? (x > y ? x : y) : (x < y ? x : y); };
+  v = f(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false));  // quad_perm 1,0,3,2
+  v = f(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false));  // quad_perm 2,3,0,1
+  v = f(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false)); // row_half_mirror
+  v = f(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false)); // row_mirror
+  return f(f(readlane(v, 0), readlane(v, 16)), f(readlane(v, 32), readlane(v, 48)));
+}
+
+template <bool kVerify>
+__global__ __launch_bounds__(kThreads) void crc32c_lane_kernel(SpanBatch a) {
+  const uint32_t n = (uint32_t)a.n;  // host cuts batches at kMaxGenericSpans (2^30)
+  __shared__ uint32_t lds[kTabWords];
+  const uint32_t tid = threadIdx.x;
+  load_slice_tables(lds, a.tabs, tid);
+  const uint32_t lane = tid & 63u;
+  __syncthreads();
+  const StrideLanes tab = stride_lanes(lane);
+  const uint32_t wave = rfl(blockIdx.x * kWavesPerGroup + (tid >> 6));
+  const uint32_t nwaves = gridDim.x * kWavesPerGroup;
+  const uint8_t* const qrun = a.qrun;
+  auto next_run = [&](uint32_t rb) -> uint32_t {  // first owned run at or after rb
+    while (rb < n && const_byte(qrun, (uint64_t)(rb >> 6)) == 0u) rb += 64u * nwaves;
+    return rb;
+  };
+  const uint32_t first = next_run(wave * 64u);
+  if (first >= n) return;
+  const bool hdr = (a.flags & kFlagLogHeader) != 0;
+  const bool has_init = a.init != nullptr;
+  // lanes without a record of the kernel's read a 2 KiB zero region (per wave)
+  const uint64_t zero = reinterpret_cast<uint64_t>(&a.tabs->zero[0]) + 2048u * (wave & 31u);
+  const uint64_t base = reinterpret_cast<uint64_t>(a.base);
+
+  // descriptors of run rb, lane's record (clamped to the last record)
+  uint64_t noff = 0;
+  uint32_t nlen = 0, ninit = 0;
+  auto fetch_desc = [&](uint32_t rb) {
+    const uint32_t i = rb < n && rb + lane < n ? rb + lane : n - 1u;
+    noff = asm_load_u64(reinterpret_cast<uint64_t>(a.off + i));
+    nlen = asm_load_u32(reinterpret_cast<uint64_t>(a.len + i));
+    if (has_init) ninit = asm_load_u32(reinterpret_cast<uint64_t>(a.init + i));
+  };
+  fetch_desc(first);
+  asm volatile("s_waitcnt vmcnt(0)" : "+v"(noff), "+v"(nlen), "+v"(ninit) : : "memory");
+
+  // issue state of the run being issued: record and body addresses, last
+  // body load offset, n4 | h << 16 | T << 18 | owned << 22, init
+  uint64_t vp = zero, vb = zero;
+  uint32_t vlen = 0, vlast = 0, vmeta = 0, vinit = 0;
+  // Per slot: body loads, head dword (first task of a run), the record's last
+  // 16 bytes (last task), stored crc (verify), and the fold's per-lane copies
+  // (record address, meta, init).  Compile-time slot indices only (the loop
+  // is unrolled over the slots).
+  u32x4 W[2][8], EV[2];
+  uint32_t HD[2] = {0u, 0u}, SC[2] = {0u, 0u}, META[2], INIT[2];
+  uint64_t VP[2];
+  auto issue = [&](LaneTask& t, int sl) {
+    if (t.rb < n && t.k == 0) {
+      const uint32_t rec = t.rb + lane;
+      const bool owned = rec < n && lane_owns(nlen, noff);
+      vp = owned ? base + noff : zero;
+      vlen = owned ? nlen : 0u;
+      const uint32_t h = (0u - (uint32_t)vp) & 3u;  // head bytes up to 4-B alignment
+      const uint32_t nc = owned ? (vlen - h) >> 4 : 0u;  // 16-B body chunks (>= 1)
+      vb = vp + h;
+      vlast = nc ? 16u * (nc - 1u) : 0u;
+      vinit = ninit;
+      const uint32_t n4 = 4u * nc;
+      vmeta = n4 | (h << 16) | (((vlen - h) & 15u) << 18) | ((owned ? 1u : 0u) << 22);
+      uint32_t K = wave_reduce<0>((n4 + 31u) >> 5);
+      uint32_t kf = wave_reduce<1>(owned ? n4 >> 5 : 0xFFFFu);
+      K = K ? K : 1u;
+      t.K = K;
+      t.kf = kf < K ? kf : K;
+      t.nrb = next_run(t.rb + 64u * nwaves);
+    }
+    // Every issue makes the same loads, so that no asm-loaded register is
+    // written under a branch (hipcc copies such registers at the merge, before
+    // their wait): the next run's descriptors again (cache hits), the head
+    // dword, the last 16 bytes and the stored crc, from the zero region unless
+    // this task needs them.
+    fetch_desc(t.nrb);
+    const bool live = t.rb < n;
+    const bool owned = live && ((vmeta >> 22) & 1u);
+    const bool lastk = t.k + 1u == t.K;
+    VP[sl] = vp;
+    META[sl] = live ? vmeta : 0u;
+    INIT[sl] = vinit;
+    HD[sl] = asm_load_u32(owned && t.k == 0 ? vp & ~3ull : zero);
+    EV[sl] = asm_load_x4(owned && lastk ? vp + vlen - 16u : zero);
+    if (kVerify) SC[sl] = asm_load_u32(owned && lastk ? (hdr ? vp - kLogCrcBack : vp + vlen) : zero);
+    // [b + min(128k + 16j, last), +16): unclamped while every record of the
+    // run covers the task, else clamped onto the record's last body chunk
+    const uint64_t b = live ? vb : zero;
+    const uint32_t k128 = 128u * t.k;
+    const uint32_t last = !live ? 0u : (t.k < t.kf ? 0xFFFFu : vlast);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t o = k128 + 16u * (uint32_t)j;
+      W[sl][j] = asm_load_x4((b + (o < last ? o : last)) & ~(uint64_t)PRISMDB_LANE_ALIGNED);
+    }
+  };
+  auto next = [&](const LaneTask& t) -> LaneTask {
+    LaneTask u = t;
+    if (t.rb >= n) return u;
+    if (t.k + 1u < t.K) {
+      u.k = t.k + 1u;
+    } else {
+      u.rb = t.nrb;
+      u.k = 0;
+      u.K = 1;
+      u.kf = 0;
+    }
+    return u;
+  };
+
+  uint32_t acc = 0;
+  auto fold = [&](const LaneTask& t, int sl) {
+    const u32x4(&w)[8] = W[sl];
+    const uint32_t meta = META[sl];
+    const uint32_t n4 = meta & 0xFFFFu;
+    // byte step: shift_1(r ^ b) = (r ^ b) >> 8 ^ slice4[3][(r ^ b) & 255]
+    auto byte_step = [&](uint32_t r, uint32_t bt) -> uint32_t {
+      const uint32_t y = r ^ bt;
+      return lds_word(lds, __builtin_amdgcn_perm(y, tab.L[3], 0x0C020400u)) ^ (y >> 8);
+    };
+    uint32_t r0 = 0u;  // first task: the register after the head bytes
+    if (t.k == 0) {
+      const uint32_t h = (meta >> 16) & 3u;
+      const uint32_t hb = HD[sl] >> (8u * ((4u - h) & 3u));  // the record's first bytes
+      uint32_t r = INIT[sl] ^ kConditioning;
+#pragma unroll
+      for (uint32_t i = 0; i < 3; ++i) {
+        const uint32_t v = byte_step(r, (hb >> (8u * i)) & 255u);
+        r = i < h ? v : r;
+      }
+      r0 = r;
+    }
+    const uint32_t done = 32u * t.k;
+    const uint32_t rem = n4 > done ? n4 - done : 0u;  // the lane's body words left at this task
+    // the register enters with body word 0 (every record of the kernel has >= 4)
+    const uint32_t x0 = t.k == 0 ? r0 ^ w[0].x : step256(lds, tab, acc, w[0].x);
+    uint32_t x;
+    if (PRISMDB_LANE_NOFOLD) {
+      x = x0;
+#pragma unroll
+      for (int i = 1; i < 32; ++i) x ^= w[i >> 2][i & 3];
+    } else if (t.k < t.kf) {
+      x = x0;
+#pragma unroll
+      for (int i = 1; i < 32; ++i) x = step256(lds, tab, x, w[i >> 2][i & 3]);
+    } else {
+      x = rem > 0u ? x0 : acc;
+#pragma unroll
+      for (int i = 1; i < 32; ++i) {
+        const uint32_t y = step256(lds, tab, x, w[i >> 2][i & 3]);
+        x = rem > (uint32_t)i ? y : x;
+      }
+    }
+    acc = x;
+    if (t.k + 1u == t.K) {
+      uint32_t r = step256(lds, tab, x, 0u);  // shift_4 after the last body word
+      // tail: tw words, then tb bytes, all inside the last 16 bytes ev; the
+      // j-th word from the end sits at dwords (4 - j, 3 - j) shifted by 4 - tb
+      const u32x4 ev = EV[sl];
+      const uint32_t T = (meta >> 18) & 15u, tw = T >> 2, tb = T & 3u;
+      const uint32_t sh = (4u - tb) & 3u;
+      const uint32_t tw3 = tb ? __builtin_amdgcn_alignbyte(ev.y, ev.x, sh) : ev.y;
+      const uint32_t tw2 = tb ? __builtin_amdgcn_alignbyte(ev.z, ev.y, sh) : ev.z;
+      const uint32_t tw1 = tb ? __builtin_amdgcn_alignbyte(ev.w, ev.z, sh) : ev.w;
+      r = tw >= 3u ? step256(lds, tab, r ^ tw3, 0u) : r;
+      r = tw >= 2u ? step256(lds, tab, r ^ tw2, 0u) : r;
+      r = tw >= 1u ? step256(lds, tab, r ^ tw1, 0u) : r;
+      const uint32_t fb = tb ? ev.w >> (8u * (4u - tb)) : 0u;
+#pragma unroll
+      for (uint32_t i = 0; i < 3; ++i) {
+        const uint32_t v = byte_step(r, (fb >> (8u * i)) & 255u);
+        r = i < tb ? v : r;
+      }
+      const uint32_t crc = r ^ kConditioning;
+      const uint32_t v = (a.flags & kFlagMask) ? mask_crc(crc) : crc;
+      if ((meta >> 22) & 1u) {
+        const uint32_t rec = t.rb + lane;
+        const uint32_t len = ((meta >> 16) & 3u) + 4u * n4 + T;
+        if ((a.flags & kFlagWriteTrailer))
+          store_le32(reinterpret_cast<const uint8_t*>(hdr ? VP[sl] - kLogCrcBack : VP[sl] + len), v);
+        if (a.out != nullptr) __builtin_nontemporal_store(v, a.out + rec);
+        if (kVerify && a.mismatch != nullptr)
+          __builtin_nontemporal_store((uint8_t)(crc != unmask_crc(SC[sl]) ? 1u : 0u), a.mismatch + rec);
+      }
+    }
+  };
+
+  LaneTask tk[2];
+  tk[0] = LaneTask{first, 0u, 0u, 1u, n};
+  issue(tk[0], 0);
+  // the next run's descriptors (issued before the eight body loads) may be
+  // read by the second issue: retire everything but those eight loads
+  asm volatile("s_waitcnt vmcnt(8)" : "+v"(noff), "+v"(nlen), "+v"(ninit), "+v"(HD[0]), "+v"(EV[0]), "+v"(SC[0]) : : "memory");
+  tk[1] = next(tk[0]);
+  issue(tk[1], 1);
+  for (;;) {
+#pragma unroll
+    for (int sl = 0; sl < 2; ++sl) {
+      wait_lane(W[sl], HD[sl], EV[sl], SC[sl], noff, nlen, ninit);
+      if (tk[sl].rb < n) fold(tk[sl], sl);
+      if (tk[sl ^ 1].rb >= n) goto drained;
+      tk[sl] = next(tk[sl ^ 1]);
+      issue(tk[sl], sl);
+    }
+  }
+drained:
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int sl = 0; sl < 2; ++sl) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) asm volatile("" : "+v"(W[sl][j]));
+    asm volatile("" : "+v"(HD[sl]), "+v"(EV[sl]), "+v"(SC[sl]));
+  }
+  asm volatile("" : "+v"(noff), "+v"(nlen), "+v"(ninit));
+}
+
 // The spans the quad kernel leaves to the generic path (len > kQuadMaxLen, or
 // outside their task's window), listed run by run (a wave's 64 consecutive
 // spans stay together and in order); ws.counters->nlist is the count.  One
 // atomic per block of 16 runs (one per run serialized on the counter: 790 us
 // for 64 Ki runs).  ws.qrun[r] = 1 if the quad kernel owns a span of run r:
 // it skips the other runs.
+template <bool kLane>  // kLane: the lane kernel's criterion (lane_owns), else the quad kernel's window
 __global__ __launch_bounds__(kListThreads) void crc32c_long_list_kernel(SpanBatch a, SplitWs ws) {
   const uint64_t n = a.n;
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
@@ -1884,20 +2214,26 @@ __global__ __launch_bounds__(kListThreads) void crc32c_long_list_kernel(SpanBatc
   const uint64_t step = (uint64_t)gridDim.x * kListThreads;
   for (uint64_t b0 = (uint64_t)blockIdx.x * kListThreads; b0 < n; b0 += step) {
     const uint64_t i = b0 + 64u * wv + lane;
-    // the task (4-aligned quad of records) this lane's record belongs to
-    const uint64_t t0 = i & ~3ull;
-    uint64_t off[4];
-    uint32_t len[4], valid = 0u;
+    bool mine;
+    if constexpr (kLane) {
+      const uint64_t ic = i < n ? i : n - 1u;
+      mine = i < n && lane_owns(a.len[ic], a.off[ic]);
+    } else {
+      // the task (4-aligned quad of records) this lane's record belongs to
+      const uint64_t t0 = i & ~3ull;
+      uint64_t off[4];
+      uint32_t len[4], valid = 0u;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const uint64_t r = t0 + (uint64_t)q;
-      const uint64_t rc = r < n ? r : n - 1u;
-      off[q] = a.off[rc];
-      len[q] = a.len[rc];
-      valid |= (r < n ? 1u : 0u) << q;
+      for (int q = 0; q < 4; ++q) {
+        const uint64_t r = t0 + (uint64_t)q;
+        const uint64_t rc = r < n ? r : n - 1u;
+        off[q] = a.off[rc];
+        len[q] = a.len[rc];
+        valid |= (r < n ? 1u : 0u) << q;
+      }
+      const QuadWindow win = quad_window(a.base, off, len, valid);
+      mine = i < n && ((win.mask >> (i & 3u)) & 1u);
     }
-    const QuadWindow win = quad_window(a.base, off, len, valid);
-    const bool mine = i < n && ((win.mask >> (i & 3u)) & 1u);
     const bool lng = i < n && !mine;
     const uint64_t m = __ballot(lng);
     const uint64_t own = __ballot(mine);
@@ -1983,9 +2319,16 @@ hipError_t launch_slices(const SpanBatch& a, const SplitWs& ws, hipStream_t s) {
 
 hipError_t launch_quad(const SpanBatch& a, bool verify, int grid, const SplitWs& ws, hipStream_t s) {
   const uint64_t lb = (a.n + kListThreads - 1) / kListThreads;
-  crc32c_long_list_kernel<<<(int)(lb < 1024u ? lb : 1024u), kListThreads, 0, s>>>(a, ws);
-  if (verify) crc32c_quad_kernel<true><<<grid, kThreads, 0, s>>>(a);
-  else crc32c_quad_kernel<false><<<grid, kThreads, 0, s>>>(a);
+  const int lgrid = (int)(lb < 1024u ? lb : 1024u);
+  if (PRISMDB_LANE_KERNEL) {
+    crc32c_long_list_kernel<true><<<lgrid, kListThreads, 0, s>>>(a, ws);
+    if (verify) crc32c_lane_kernel<true><<<grid, kThreads, 0, s>>>(a);
+    else crc32c_lane_kernel<false><<<grid, kThreads, 0, s>>>(a);
+  } else {
+    crc32c_long_list_kernel<false><<<lgrid, kListThreads, 0, s>>>(a, ws);
+    if (verify) crc32c_quad_kernel<true><<<grid, kThreads, 0, s>>>(a);
+    else crc32c_quad_kernel<false><<<grid, kThreads, 0, s>>>(a);
+  }
   return hipGetLastError();
 }
 

@@ -62,6 +62,8 @@ VARIANTS = {
     "noedge": {"PRISMDB_SPAN_NOEDGE": 1, "PRISMDB_MEASURE_ONLY": 1},
     # measurement: fixed kernel pairs spans half a run apart, like the span kernel's two streams
     "far_pair": {"PRISMDB_FIXED_FAR_PAIR": 1},
+    # measurement: fixed kernel folds a pair as ONE dependent chain of 2K rounds (wrong results)
+    "chain": {"PRISMDB_FIXED_CHAIN": 1, "PRISMDB_MEASURE_ONLY": 1},
     # span kernel: streams in their own runs even when every record is one task (round 1)
     "no_pair_runs": {"PRISMDB_SPAN_PAIR_RUNS": 0},
     # planner: a long span's thread writes its segment records alone (as in round 1)
@@ -79,6 +81,13 @@ VARIANTS = {
     # span kernel runs mode (one-task records): 16 runs per stream (round 1) / 256
     "runs16": {"PRISMDB_RUNS_PER_STREAM": 16},
     "runs256": {"PRISMDB_RUNS_PER_STREAM": 256},
+    # log batches through the quad kernel (four records per wave) instead of the lane kernel
+    "quadk": {"PRISMDB_LANE_KERNEL": 0},
+    # measurement-only: lane kernel loads without the fold / with 16-B aligned body loads (wrong results)
+    "lane_nofold": {"PRISMDB_LANE_NOFOLD": 1, "PRISMDB_MEASURE_ONLY": 1},
+    "lane_aligned": {"PRISMDB_LANE_ALIGNED": 15, "PRISMDB_MEASURE_ONLY": 1},
+    "lane_aligned4": {"PRISMDB_LANE_ALIGNED": 3, "PRISMDB_MEASURE_ONLY": 1},
+    "lane_aligned8": {"PRISMDB_LANE_ALIGNED": 7, "PRISMDB_MEASURE_ONLY": 1},
     # quad kernel ring depth (tasks in flight + 1)
     "quad_r2": {"PRISMDB_QUAD_RING": 2},
     "quad_r3": {"PRISMDB_QUAD_RING": 3},
@@ -201,6 +210,8 @@ def do_run(args, names):
         e1.synchronize()
         return e0.elapsed_time(e1) / 1e3 / k
 
+    if args.work:
+        work = {w: v for w, v in work.items() if w in args.work}
     res = {w: {n: [] for n in names} for w in work}
     agree = {}
     outs_of = {"wal": wout, "sst3988": sout, "huge64m": hout, "file_fixed": fout, "file_desc": fout}
@@ -237,6 +248,7 @@ def main():
     ap.add_argument("--gib", type=int, default=64)
     ap.add_argument("--reps", type=int, default=8)
     ap.add_argument("--only", nargs="*")
+    ap.add_argument("--work", nargs="*", help="workloads to time (default: all)")
     args = ap.parse_args()
     names = args.only or list(VARIANTS)
     if args.mode == "build":
