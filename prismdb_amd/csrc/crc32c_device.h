@@ -69,12 +69,9 @@ constexpr uint32_t kQuadBack = kQuadMaxLen;
 #ifndef PRISMDB_LANE_KERNEL
 #define PRISMDB_LANE_KERNEL 1
 #endif
-constexpr uint32_t kLaneMinLen = 20u;   // >= 3 head bytes + one 16-B body chunk + the 16-B tail load
+constexpr uint32_t kLaneMinLen = 8u;  // >= 3 head bytes + one body word
 constexpr uint32_t kLaneMaxLen = 1280u;
-// off >= 3: the head dword (4-B aligned, at or below the record) stays in the buffer
-__host__ __device__ constexpr bool lane_owns(uint32_t len, uint64_t off) {
-  return len >= kLaneMinLen && len <= kLaneMaxLen && off >= 3u;
-}
+__host__ __device__ constexpr bool lane_owns(uint32_t len) { return len >= kLaneMinLen && len <= kLaneMaxLen; }
 
 enum : uint32_t { kRoleSpans = 0, kRoleSegments = 1 };
 

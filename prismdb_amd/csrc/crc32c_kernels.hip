@@ -80,9 +80,6 @@
 #ifndef PRISMDB_LANE_NOFOLD  // measurement knob: lane kernel XORs its words instead of folding them (wrong results)
 #define PRISMDB_LANE_NOFOLD 0
 #endif
-#ifndef PRISMDB_LANE_ALIGNED  // measurement knob: lane kernel body load addresses & ~this (15: 16-B aligned; wrong results)
-#define PRISMDB_LANE_ALIGNED 0
-#endif
 #ifndef PRISMDB_SPAN_NOEDGE  // measurement knob: span kernel issues no edge-byte load (wrong with tails / verify)
 #define PRISMDB_SPAN_NOEDGE 0
 #endif
@@ -1907,21 +1904,22 @@ __global__ __launch_bounds__(kThreads) void crc32c_quad_kernel(SpanBatch a) {
 // and v_perm addresses as the stride tables) -- the same lookups per byte as
 // the wave-wide fold, with no realignment, no cross-lane reduction and no
 // per-record scalar work.  A record is h <= 3 head bytes up to 4-B
-// alignment, then 16-B chunks (read with 4-B aligned 16-B loads: byte-
-// unaligned ones measured 16 % slower), then T <= 15 tail bytes.  The head
-// bytes come from the aligned dword holding the record's first byte, the tail
-// from one 16-B load ending at the record's end: its words funnel-shifted out
-// at fixed dword positions from the end, its last T % 4 bytes the top bytes
-// of its last dword.  Bytes go through byte steps (shift_1(y) = y >> 8 ^
-// slice4[3][y & 255]).
+// alignment, n4 body words, then tb <= 3 tail bytes.  The body is read in
+// whole 128-B lines (eight 16-B loads per lane and task, line-aligned): a lane
+// fetches each line of its record once, in one task.  (Loads that followed
+// the record's own alignment straddled two lines per task and fetched
+// 1.86 x the record bytes from HBM -- PMC FETCH_SIZE -- the lines refetched
+// by the next task after L2 had evicted them.)  Words of the first and last
+// lines outside the body are masked; a line holding a byte of the record
+// lies in a mapped page, so reading all of it is safe.  The head bytes come
+// from the aligned dword holding the record's first byte, the tail bytes are
+// the top bytes of the dword ending the record; both go through byte steps
+// (shift_1(y) = y >> 8 ^ slice4[3][y & 255]).
 //
-// A task is 128 B of every lane's chunks: eight global_load_dwordx4, issued
-// one task ahead into a two-slot ring and retired by counted vmcnt waits.
-// Tasks before the run's shortest record ends fold unmasked; later ones keep
-// a lane's register past its last word and clamp its loads onto the record's
-// last chunk (every load stays inside the record).
-// Records of kLaneMinLen..kLaneMaxLen bytes are the kernel's (lane_owns);
-// the long-span list sends the rest down the generic path.
+// A task is one 128-B line of every lane's record, issued one task ahead into
+// a two-slot ring and retired by counted vmcnt waits.  Task 0 (where bodies
+// start) and tasks past the run's shortest record fold under per-word masks,
+// the others unmasked; a lane past its record re-reads its last line.
 //
 // Load order inside an issue: the next run's descriptors (first task of a
 // run), the run's edge dwords (last task), then the eight body loads, so the
@@ -1940,6 +1938,14 @@ __device__ __forceinline__ u32x4 asm_load_x4(uint64_t addr) {
   asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(r) : "v"(addr));
   return r;
 }
+// One 128-B line (lane kernel body): eight 16-B loads at immediate offsets.
+template <int J = 0>
+__device__ __forceinline__ void asm_load_line(u32x4 (&w)[8], uint64_t addr) {
+  if constexpr (J < 8) {
+    asm volatile("global_load_dwordx4 %0, %1, off offset:%2" : "=v"(w[J]) : "v"(addr), "n"(16 * J));
+    asm_load_line<J + 1>(w, addr);
+  }
+}
 template <int kImm>
 __device__ __forceinline__ u32x4 asm_load_x4_at(uint64_t addr) {
   u32x4 r;
@@ -1957,14 +1963,15 @@ __device__ __forceinline__ uint64_t asm_load_u64(uint64_t addr) {
   return r;
 }
 
-// Wait for a slot's loads (w: body, hd: head dword, ev: the record's last
-// 16 bytes, sc: stored crc) with the other slot's eight body loads in flight;
-// the slot's registers and the prefetched descriptors are in/out operands.
-__device__ __forceinline__ void wait_lane(u32x4 (&w)[8], uint32_t& hd, u32x4& ev, uint32_t& sc, uint64_t& noff,
+// Wait for a slot's loads (w: body line, hd: head dword, ed: the dword ending
+// the record, sc: stored crc) with the other slot's eight body loads in
+// flight; the slot's registers and the prefetched descriptors are in/out
+// operands.
+__device__ __forceinline__ void wait_lane(u32x4 (&w)[8], uint32_t& hd, uint32_t& ed, uint32_t& sc, uint64_t& noff,
                                           uint32_t& nlen, uint32_t& ninit) {
   asm volatile("s_waitcnt vmcnt(8)"
                : "+v"(w[0]), "+v"(w[1]), "+v"(w[2]), "+v"(w[3]), "+v"(w[4]), "+v"(w[5]), "+v"(w[6]),
-                 "+v"(w[7]), "+v"(hd), "+v"(ev), "+v"(sc), "+v"(noff), "+v"(nlen), "+v"(ninit)
+                 "+v"(w[7]), "+v"(hd), "+v"(ed), "+v"(sc), "+v"(noff), "+v"(nlen), "+v"(ninit)
                :
                : "memory");
 }
@@ -2021,62 +2028,58 @@ __global__ __launch_bounds__(kThreads) void crc32c_lane_kernel(SpanBatch a) {
   fetch_desc(first);
   asm volatile("s_waitcnt vmcnt(0)" : "+v"(noff), "+v"(nlen), "+v"(ninit) : : "memory");
 
-  // issue state of the run being issued: record and body addresses, last
-  // body load offset, n4 | h << 16 | T << 18 | owned << 22, init
-  uint64_t vp = zero, vb = zero;
-  uint32_t vlen = 0, vlast = 0, vmeta = 0, vinit = 0;
-  // Per slot: body loads, head dword (first task of a run), the record's last
-  // 16 bytes (last task), stored crc (verify), and the fold's per-lane copies
-  // (record address, meta, init).  Compile-time slot indices only (the loop
-  // is unrolled over the slots).
-  u32x4 W[2][8], EV[2];
-  uint32_t HD[2] = {0u, 0u}, SC[2] = {0u, 0u}, META[2], INIT[2];
+  // issue state of the run being issued: record address, the line holding
+  // the body's first word, the lane's last task (line), n4 | q0 << 16 | h << 21
+  // | tb << 23 | owned << 25 (q0: the body's first word in that line), init
+  uint64_t vp = zero, vl = zero;
+  uint32_t vlen = 0, vkend = 0, vmeta = 0, vinit = 0;
+  // Per slot: the body line, head dword (first task of a run), the dword
+  // ending the record (last task), stored crc (verify), and the fold's
+  // per-lane copies (record address, meta, init).  Compile-time slot indices
+  // only (the loop is unrolled over the slots).
+  u32x4 W[2][8];
+  uint32_t HD[2] = {0u, 0u}, ED[2] = {0u, 0u}, SC[2] = {0u, 0u}, META[2], INIT[2];
   uint64_t VP[2];
   auto issue = [&](LaneTask& t, int sl) {
     if (t.rb < n && t.k == 0) {
       const uint32_t rec = t.rb + lane;
-      const bool owned = rec < n && lane_owns(nlen, noff);
+      const bool owned = rec < n && lane_owns(nlen);
       vp = owned ? base + noff : zero;
       vlen = owned ? nlen : 0u;
-      const uint32_t h = (0u - (uint32_t)vp) & 3u;  // head bytes up to 4-B alignment
-      const uint32_t nc = owned ? (vlen - h) >> 4 : 0u;  // 16-B body chunks (>= 1)
-      vb = vp + h;
-      vlast = nc ? 16u * (nc - 1u) : 0u;
+      const uint32_t h = owned ? (0u - (uint32_t)vp) & 3u : 0u;  // head bytes up to 4-B alignment
+      const uint32_t n4 = owned ? (vlen - h) >> 2 : 0u;          // >= 1
+      const uint32_t tb = owned ? (vlen - h) & 3u : 0u;
+      const uint64_t vb = vp + h;
+      vl = vb & ~127ull;
+      const uint32_t q0 = owned ? (uint32_t)(vb & 127u) >> 2 : 0u;
+      const uint32_t qe = q0 + n4;  // one past the body's last word, in words from vl
+      vkend = owned ? (qe + 31u) >> 5 : 1u;
       vinit = ninit;
-      const uint32_t n4 = 4u * nc;
-      vmeta = n4 | (h << 16) | (((vlen - h) & 15u) << 18) | ((owned ? 1u : 0u) << 22);
-      uint32_t K = wave_reduce<0>((n4 + 31u) >> 5);
-      uint32_t kf = wave_reduce<1>(owned ? n4 >> 5 : 0xFFFFu);
-      K = K ? K : 1u;
+      vmeta = n4 | (q0 << 16) | (h << 21) | (tb << 23) | ((owned ? 1u : 0u) << 25);
+      uint32_t K = wave_reduce<0>(vkend);
+      uint32_t kf = wave_reduce<1>(owned ? qe >> 5 : 0xFFFFu);
       t.K = K;
       t.kf = kf < K ? kf : K;
       t.nrb = next_run(t.rb + 64u * nwaves);
     }
     // Every issue makes the same loads, so that no asm-loaded register is
     // written under a branch (hipcc copies such registers at the merge, before
-    // their wait): the next run's descriptors again (cache hits), the head
-    // dword, the last 16 bytes and the stored crc, from the zero region unless
-    // this task needs them.
+    // their wait): the next run's descriptors again (cache hits), the head and
+    // end dwords and the stored crc, from the zero region unless this task
+    // needs them.
     fetch_desc(t.nrb);
     const bool live = t.rb < n;
-    const bool owned = live && ((vmeta >> 22) & 1u);
+    const bool owned = live && ((vmeta >> 25) & 1u);
     const bool lastk = t.k + 1u == t.K;
     VP[sl] = vp;
     META[sl] = live ? vmeta : 0u;
     INIT[sl] = vinit;
     HD[sl] = asm_load_u32(owned && t.k == 0 ? vp & ~3ull : zero);
-    EV[sl] = asm_load_x4(owned && lastk ? vp + vlen - 16u : zero);
+    ED[sl] = asm_load_u32(owned && lastk ? vp + vlen - 4u : zero);
     if (kVerify) SC[sl] = asm_load_u32(owned && lastk ? (hdr ? vp - kLogCrcBack : vp + vlen) : zero);
-    // [b + min(128k + 16j, last), +16): unclamped while every record of the
-    // run covers the task, else clamped onto the record's last body chunk
-    const uint64_t b = live ? vb : zero;
-    const uint32_t k128 = 128u * t.k;
-    const uint32_t last = !live ? 0u : (t.k < t.kf ? 0xFFFFu : vlast);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const uint32_t o = k128 + 16u * (uint32_t)j;
-      W[sl][j] = asm_load_x4((b + (o < last ? o : last)) & ~(uint64_t)PRISMDB_LANE_ALIGNED);
-    }
+    // line min(k, kend - 1) of the lane's record (a finished lane re-reads its last)
+    const uint32_t kl = live ? (t.k < vkend ? t.k : vkend - 1u) : 0u;
+    asm_load_line(W[sl], (live ? vl : zero) + 128u * kl);
   };
   auto next = [&](const LaneTask& t) -> LaneTask {
     LaneTask u = t;
@@ -2096,15 +2099,20 @@ __global__ __launch_bounds__(kThreads) void crc32c_lane_kernel(SpanBatch a) {
   auto fold = [&](const LaneTask& t, int sl) {
     const u32x4(&w)[8] = W[sl];
     const uint32_t meta = META[sl];
-    const uint32_t n4 = meta & 0xFFFFu;
+    const uint32_t n4 = meta & 0xFFFFu, q0 = (meta >> 16) & 31u;
     // byte step: shift_1(r ^ b) = (r ^ b) >> 8 ^ slice4[3][(r ^ b) & 255]
     auto byte_step = [&](uint32_t r, uint32_t bt) -> uint32_t {
       const uint32_t y = r ^ bt;
       return lds_word(lds, __builtin_amdgcn_perm(y, tab.L[3], 0x0C020400u)) ^ (y >> 8);
     };
-    uint32_t r0 = 0u;  // first task: the register after the head bytes
-    if (t.k == 0) {
-      const uint32_t h = (meta >> 16) & 3u;
+    uint32_t x = acc;
+    if (PRISMDB_LANE_NOFOLD) {
+#pragma unroll
+      for (int i = 0; i < 32; ++i) x ^= w[i >> 2][i & 3];
+    } else if (t.k == 0) {
+      // the head bytes, then the body from word q0 of the line: the register
+      // enters with body word 0
+      const uint32_t h = (meta >> 21) & 3u;
       const uint32_t hb = HD[sl] >> (8u * ((4u - h) & 3u));  // the record's first bytes
       uint32_t r = INIT[sl] ^ kConditioning;
 #pragma unroll
@@ -2112,44 +2120,28 @@ __global__ __launch_bounds__(kThreads) void crc32c_lane_kernel(SpanBatch a) {
         const uint32_t v = byte_step(r, (hb >> (8u * i)) & 255u);
         r = i < h ? v : r;
       }
-      r0 = r;
-    }
-    const uint32_t done = 32u * t.k;
-    const uint32_t rem = n4 > done ? n4 - done : 0u;  // the lane's body words left at this task
-    // the register enters with body word 0 (every record of the kernel has >= 4)
-    const uint32_t x0 = t.k == 0 ? r0 ^ w[0].x : step256(lds, tab, acc, w[0].x);
-    uint32_t x;
-    if (PRISMDB_LANE_NOFOLD) {
-      x = x0;
 #pragma unroll
-      for (int i = 1; i < 32; ++i) x ^= w[i >> 2][i & 3];
+      for (int i = 0; i < 32; ++i) {
+        const uint32_t rel = (uint32_t)i - q0;  // body word index (huge before the body)
+        const uint32_t y = rel == 0u ? r ^ w[i >> 2][i & 3] : step256(lds, tab, x, w[i >> 2][i & 3]);
+        x = rel < n4 ? y : x;
+      }
     } else if (t.k < t.kf) {
-      x = x0;
 #pragma unroll
-      for (int i = 1; i < 32; ++i) x = step256(lds, tab, x, w[i >> 2][i & 3]);
+      for (int i = 0; i < 32; ++i) x = step256(lds, tab, x, w[i >> 2][i & 3]);
     } else {
-      x = rem > 0u ? x0 : acc;
+      const uint32_t rel0 = 32u * t.k - q0;  // body word index of the line's word 0
 #pragma unroll
-      for (int i = 1; i < 32; ++i) {
+      for (int i = 0; i < 32; ++i) {
         const uint32_t y = step256(lds, tab, x, w[i >> 2][i & 3]);
-        x = rem > (uint32_t)i ? y : x;
+        x = rel0 + (uint32_t)i < n4 ? y : x;
       }
     }
     acc = x;
     if (t.k + 1u == t.K) {
       uint32_t r = step256(lds, tab, x, 0u);  // shift_4 after the last body word
-      // tail: tw words, then tb bytes, all inside the last 16 bytes ev; the
-      // j-th word from the end sits at dwords (4 - j, 3 - j) shifted by 4 - tb
-      const u32x4 ev = EV[sl];
-      const uint32_t T = (meta >> 18) & 15u, tw = T >> 2, tb = T & 3u;
-      const uint32_t sh = (4u - tb) & 3u;
-      const uint32_t tw3 = tb ? __builtin_amdgcn_alignbyte(ev.y, ev.x, sh) : ev.y;
-      const uint32_t tw2 = tb ? __builtin_amdgcn_alignbyte(ev.z, ev.y, sh) : ev.z;
-      const uint32_t tw1 = tb ? __builtin_amdgcn_alignbyte(ev.w, ev.z, sh) : ev.w;
-      r = tw >= 3u ? step256(lds, tab, r ^ tw3, 0u) : r;
-      r = tw >= 2u ? step256(lds, tab, r ^ tw2, 0u) : r;
-      r = tw >= 1u ? step256(lds, tab, r ^ tw1, 0u) : r;
-      const uint32_t fb = tb ? ev.w >> (8u * (4u - tb)) : 0u;
+      const uint32_t tb = (meta >> 23) & 3u;
+      const uint32_t fb = tb ? ED[sl] >> (8u * (4u - tb)) : 0u;  // the record's last tb bytes
 #pragma unroll
       for (uint32_t i = 0; i < 3; ++i) {
         const uint32_t v = byte_step(r, (fb >> (8u * i)) & 255u);
@@ -2157,9 +2149,9 @@ __global__ __launch_bounds__(kThreads) void crc32c_lane_kernel(SpanBatch a) {
       }
       const uint32_t crc = r ^ kConditioning;
       const uint32_t v = (a.flags & kFlagMask) ? mask_crc(crc) : crc;
-      if ((meta >> 22) & 1u) {
+      if ((meta >> 25) & 1u) {
         const uint32_t rec = t.rb + lane;
-        const uint32_t len = ((meta >> 16) & 3u) + 4u * n4 + T;
+        const uint32_t len = ((meta >> 21) & 3u) + 4u * n4 + tb;
         if ((a.flags & kFlagWriteTrailer))
           store_le32(reinterpret_cast<const uint8_t*>(hdr ? VP[sl] - kLogCrcBack : VP[sl] + len), v);
         if (a.out != nullptr) __builtin_nontemporal_store(v, a.out + rec);
@@ -2174,13 +2166,13 @@ __global__ __launch_bounds__(kThreads) void crc32c_lane_kernel(SpanBatch a) {
   issue(tk[0], 0);
   // the next run's descriptors (issued before the eight body loads) may be
   // read by the second issue: retire everything but those eight loads
-  asm volatile("s_waitcnt vmcnt(8)" : "+v"(noff), "+v"(nlen), "+v"(ninit), "+v"(HD[0]), "+v"(EV[0]), "+v"(SC[0]) : : "memory");
+  asm volatile("s_waitcnt vmcnt(8)" : "+v"(noff), "+v"(nlen), "+v"(ninit), "+v"(HD[0]), "+v"(ED[0]), "+v"(SC[0]) : : "memory");
   tk[1] = next(tk[0]);
   issue(tk[1], 1);
   for (;;) {
 #pragma unroll
     for (int sl = 0; sl < 2; ++sl) {
-      wait_lane(W[sl], HD[sl], EV[sl], SC[sl], noff, nlen, ninit);
+      wait_lane(W[sl], HD[sl], ED[sl], SC[sl], noff, nlen, ninit);
       if (tk[sl].rb < n) fold(tk[sl], sl);
       if (tk[sl ^ 1].rb >= n) goto drained;
       tk[sl] = next(tk[sl ^ 1]);
@@ -2193,7 +2185,7 @@ drained:
   for (int sl = 0; sl < 2; ++sl) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) asm volatile("" : "+v"(W[sl][j]));
-    asm volatile("" : "+v"(HD[sl]), "+v"(EV[sl]), "+v"(SC[sl]));
+    asm volatile("" : "+v"(HD[sl]), "+v"(ED[sl]), "+v"(SC[sl]));
   }
   asm volatile("" : "+v"(noff), "+v"(nlen), "+v"(ninit));
 }
@@ -2216,8 +2208,7 @@ __global__ __launch_bounds__(kListThreads) void crc32c_long_list_kernel(SpanBatc
     const uint64_t i = b0 + 64u * wv + lane;
     bool mine;
     if constexpr (kLane) {
-      const uint64_t ic = i < n ? i : n - 1u;
-      mine = i < n && lane_owns(a.len[ic], a.off[ic]);
+      mine = i < n && lane_owns(a.len[i < n ? i : n - 1u]);
     } else {
       // the task (4-aligned quad of records) this lane's record belongs to
       const uint64_t t0 = i & ~3ull;

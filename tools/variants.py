@@ -83,11 +83,9 @@ VARIANTS = {
     "runs256": {"PRISMDB_RUNS_PER_STREAM": 256},
     # log batches through the quad kernel (four records per wave) instead of the lane kernel
     "quadk": {"PRISMDB_LANE_KERNEL": 0},
-    # measurement-only: lane kernel loads without the fold / with 16-B aligned body loads (wrong results)
+    # measurement-only: lane kernel loads without the fold (wrong results); the
+    # alignment / nt probes of profiles/r02s3f, r02s3h were knobs of earlier lane-kernel builds
     "lane_nofold": {"PRISMDB_LANE_NOFOLD": 1, "PRISMDB_MEASURE_ONLY": 1},
-    "lane_aligned": {"PRISMDB_LANE_ALIGNED": 15, "PRISMDB_MEASURE_ONLY": 1},
-    "lane_aligned4": {"PRISMDB_LANE_ALIGNED": 3, "PRISMDB_MEASURE_ONLY": 1},
-    "lane_aligned8": {"PRISMDB_LANE_ALIGNED": 7, "PRISMDB_MEASURE_ONLY": 1},
     # quad kernel ring depth (tasks in flight + 1)
     "quad_r2": {"PRISMDB_QUAD_RING": 2},
     "quad_r3": {"PRISMDB_QUAD_RING": 3},
