@@ -186,6 +186,10 @@ def do_run(args, names):
         "wal": (lambda n: libs[n][1](buf.data_ptr(), woff.data_ptr(), wlen.data_ptr(), None, nw,
                                      wout.data_ptr(), wmm.data_ptr(), 0x4, sp),
                 int(hlen.sum() + len(hlen)) * nf + nw * (4 + 1 + 12)),
+        # log::Writer's header crcs, sealed in place (the same bytes: the buffer does not change)
+        "wal_seal": (lambda n: libs[n][1](buf.data_ptr(), woff.data_ptr(), wlen.data_ptr(), None, nw,
+                                          wout.data_ptr(), None, 0x7, sp),
+                     int(hlen.sum() + len(hlen)) * nf + nw * (4 + 4 + 12)),
         "sst3988": (lambda n: libs[n][1](buf.data_ptr(), soff.data_ptr(), slen.data_ptr(), None, ns,
                                          sout.data_ptr(), None, 0, sp), ns * (3988 + 4 + 12)),
         "huge64m": (lambda n: libs[n][1](buf.data_ptr(), hoff_.data_ptr(), hlen_.data_ptr(), None, nh,
@@ -212,7 +216,7 @@ def do_run(args, names):
         work = {w: v for w, v in work.items() if w in args.work}
     res = {w: {n: [] for n in names} for w in work}
     agree = {}
-    outs_of = {"wal": wout, "sst3988": sout, "huge64m": hout, "file_fixed": fout, "file_desc": fout}
+    outs_of = {"wal": wout, "wal_seal": wout, "sst3988": sout, "huge64m": hout, "file_fixed": fout, "file_desc": fout}
     for w, (fn, _) in work.items():
         ref = None
         for n in names:
