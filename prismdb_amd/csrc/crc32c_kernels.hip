@@ -74,8 +74,14 @@
 #ifndef PRISMDB_FIXED_FAR_PAIR  // measurement knob: fixed kernel pairs spans half a run apart (the span kernel's pattern)
 #define PRISMDB_FIXED_FAR_PAIR 0
 #endif
+#ifndef PRISMDB_FIXED_SETPRIO
+#define PRISMDB_FIXED_SETPRIO 0
+#endif
 #ifndef PRISMDB_FIXED_CHAIN  // measurement knob: the pair's second span starts from the first's register (one dependent chain; wrong results)
 #define PRISMDB_FIXED_CHAIN 0
+#endif
+#ifndef PRISMDB_LANE_THREADS  // lane kernel workgroup size (one group per CU)
+#define PRISMDB_LANE_THREADS 512
 #endif
 #ifndef PRISMDB_LANE_NOFOLD  // measurement knob: lane kernel XORs its words instead of folding them (wrong results)
 #define PRISMDB_LANE_NOFOLD 0
@@ -1097,8 +1103,14 @@ __global__ __launch_bounds__(kThreads) void crc32c_fixed_kernel(SpanBatch a) {
         if (nxt >= n || (nxt & (kRun - 1u)) == 0) flush();
       }
       cur = nxt;
+#if PRISMDB_FIXED_SETPRIO  // A/B knob: the pair's loads issued at raised wave priority
+      __builtin_amdgcn_s_setprio(PRISMDB_FIXED_SETPRIO);
+#endif
       issue(ahead, ring[s]);
       issue(ahead + kSecond, ring[s + 1]);
+#if PRISMDB_FIXED_SETPRIO
+      __builtin_amdgcn_s_setprio(0);
+#endif
       ahead = adv(ahead);
     }
     if (cur >= n) break;
@@ -1926,8 +1938,15 @@ __global__ __launch_bounds__(kThreads) void crc32c_quad_kernel(SpanBatch a) {
 // body loads of the other slot are always the youngest eight: after a
 // vmcnt(8) wait every descriptor and edge load issued so far has landed.
 // ---------------------------------------------------------------------------
+// Lane kernel workgroup (PRISMDB_LANE_THREADS): one group per CU either way
+// (the tables take 128 KiB of LDS).  8 waves per CU read 11.7 % faster than 16
+// and 4 % faster than 12 (WAL verify; profiles/r02s3n, r02s3o): each lane's
+// line is read by eight 16-B loads, and fewer waves keep fewer lines in flight
+// in the CU's vector L1 between them; 4 waves hide too little latency (-27 %).
+constexpr uint32_t kLaneThreads = PRISMDB_LANE_THREADS;
+
 __device__ __forceinline__ void load_slice_tables(uint32_t* lds, const DeviceTables* tabs, uint32_t tid) {
-  for (uint32_t w = tid; w < (uint32_t)kTabWords; w += kThreads) {
+  for (uint32_t w = tid; w < (uint32_t)kTabWords; w += kLaneThreads) {
     const uint32_t k = ((w >> 14) << 1) | ((w >> 5) & 1u), e = (w >> 6) & 255u;
     lds[w] = tabs->slice4[k][e];
   }
@@ -1993,7 +2012,7 @@ __device__ __forceinline__ uint32_t wave_reduce(uint32_t v) {
 }
 
 template <bool kVerify>
-__global__ __launch_bounds__(kThreads) void crc32c_lane_kernel(SpanBatch a) {
+__global__ __launch_bounds__(kLaneThreads) void crc32c_lane_kernel(SpanBatch a) {
   const uint32_t n = (uint32_t)a.n;  // host cuts batches at kMaxGenericSpans (2^30)
   __shared__ uint32_t lds[kTabWords];
   const uint32_t tid = threadIdx.x;
@@ -2001,8 +2020,8 @@ __global__ __launch_bounds__(kThreads) void crc32c_lane_kernel(SpanBatch a) {
   const uint32_t lane = tid & 63u;
   __syncthreads();
   const StrideLanes tab = stride_lanes(lane);
-  const uint32_t wave = rfl(blockIdx.x * kWavesPerGroup + (tid >> 6));
-  const uint32_t nwaves = gridDim.x * kWavesPerGroup;
+  const uint32_t wave = rfl(blockIdx.x * (kLaneThreads / 64u) + (tid >> 6));
+  const uint32_t nwaves = gridDim.x * (kLaneThreads / 64u);
   const uint8_t* const qrun = a.qrun;
   auto next_run = [&](uint32_t rb) -> uint32_t {  // first owned run at or after rb
     while (rb < n && const_byte(qrun, (uint64_t)(rb >> 6)) == 0u) rb += 64u * nwaves;
@@ -2320,8 +2339,8 @@ hipError_t launch_quad(const SpanBatch& a, bool verify, int grid, const SplitWs&
   const int lgrid = (int)(lb < 16384u ? lb : 16384u);
   if (PRISMDB_LANE_KERNEL) {
     crc32c_long_list_kernel<true><<<lgrid, kListThreads, 0, s>>>(a, ws);
-    if (verify) crc32c_lane_kernel<true><<<grid, kThreads, 0, s>>>(a);
-    else crc32c_lane_kernel<false><<<grid, kThreads, 0, s>>>(a);
+    if (verify) crc32c_lane_kernel<true><<<grid, kLaneThreads, 0, s>>>(a);
+    else crc32c_lane_kernel<false><<<grid, kLaneThreads, 0, s>>>(a);
   } else {
     crc32c_long_list_kernel<false><<<lgrid, kListThreads, 0, s>>>(a, ws);
     if (verify) crc32c_quad_kernel<true><<<grid, kThreads, 0, s>>>(a);

@@ -64,6 +64,9 @@ VARIANTS = {
     "far_pair": {"PRISMDB_FIXED_FAR_PAIR": 1},
     # measurement: fixed kernel folds a pair as ONE dependent chain of 2K rounds (wrong results)
     "chain": {"PRISMDB_FIXED_CHAIN": 1, "PRISMDB_MEASURE_ONLY": 1},
+    # fixed kernel: a pair's loads issued at wave priority 1 / 3 (s_setprio)
+    "setprio1": {"PRISMDB_FIXED_SETPRIO": 1},
+    "setprio3": {"PRISMDB_FIXED_SETPRIO": 3},
     # span kernel: streams in their own runs even when every record is one task (round 1)
     "no_pair_runs": {"PRISMDB_SPAN_PAIR_RUNS": 0},
     # planner: a long span's thread writes its segment records alone (as in round 1)
@@ -86,6 +89,13 @@ VARIANTS = {
     # measurement-only: lane kernel loads without the fold (wrong results); the
     # alignment / nt probes of profiles/r02s3f, r02s3h were knobs of earlier lane-kernel builds
     "lane_nofold": {"PRISMDB_LANE_NOFOLD": 1, "PRISMDB_MEASURE_ONLY": 1},
+    # lane kernel with 8 / 4 waves per CU (fewer record lines in flight per CU)
+    "lane_w8": {"PRISMDB_LANE_THREADS": 512},
+    "lane_w12": {"PRISMDB_LANE_THREADS": 768},
+    "lane_w6": {"PRISMDB_LANE_THREADS": 384},
+    "lane_w10": {"PRISMDB_LANE_THREADS": 640},
+    "lane_w16": {"PRISMDB_LANE_THREADS": 1024},
+    "lane_w4": {"PRISMDB_LANE_THREADS": 256},
     # quad kernel ring depth (tasks in flight + 1)
     "quad_r2": {"PRISMDB_QUAD_RING": 2},
     "quad_r3": {"PRISMDB_QUAD_RING": 3},
