@@ -1,0 +1,18 @@
+#!/bin/bash
+# Session-3 close: GPU suite, smoke, default bench, secondary workloads on HEAD
+set -o pipefail
+R=$GRAFT_REPO_ROOT; O=$R/gpurun_out; mkdir -p $O
+cd $R
+timeout -k 10 900 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 300 --timeout-method thread -x > $O/s3z_tests.log 2>&1 || { tail -20 $O/s3z_tests.log; exit 1; }
+tail -1 $O/s3z_tests.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/s3z_smoke.log 2>&1 || { tail -20 $O/s3z_smoke.log; exit 1; }
+tail -1 $O/s3z_smoke.log
+timeout -k 10 600 python bench.py > $O/s3z_bench.json 2> $O/s3z_bench.err || exit $?
+cat $O/s3z_bench.json
+timeout -k 10 600 python tools/bench_configs.py > $O/s3z_configs.json 2> $O/s3z_configs.err || { tail -20 $O/s3z_configs.err; exit 1; }
+python - <<'PY'
+import json
+d = json.load(open("gpurun_out/s3z_configs.json"))
+for w, r in d["results"].items():
+    print(w, {k: v for k, v in r.items() if k in ("GiB/s", "roofline_frac", "mismatches")})
+PY
