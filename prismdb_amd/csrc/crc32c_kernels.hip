@@ -1934,8 +1934,8 @@ __global__ __launch_bounds__(kThreads) void crc32c_quad_kernel(SpanBatch a) {
 // the others unmasked; a lane past its record re-reads its last line.
 //
 // Load order inside an issue: the next run's descriptors (first task of a
-// run), the run's edge dwords (last task), then the eight body loads, so the
-// body loads of the other slot are always the youngest eight: after a
+// run), the edge dwords (first / last task), then the eight body loads, so
+// the body loads of the other slot are always the youngest eight: after a
 // vmcnt(8) wait every descriptor and edge load issued so far has landed.
 // ---------------------------------------------------------------------------
 // Lane kernel workgroup (PRISMDB_LANE_THREADS): one group per CU either way
@@ -2081,21 +2081,28 @@ __global__ __launch_bounds__(kLaneThreads) void crc32c_lane_kernel(SpanBatch a) 
       t.kf = kf < K ? kf : K;
       t.nrb = next_run(t.rb + 64u * nwaves);
     }
-    // Every issue makes the same loads, so that no asm-loaded register is
-    // written under a branch (hipcc copies such registers at the merge, before
-    // their wait): the next run's descriptors again (cache hits), the head and
-    // end dwords and the stored crc, from the zero region unless this task
-    // needs them.
-    fetch_desc(t.nrb);
+    // Side loads: the next run's descriptors with a run's first task, the
+    // head dword with it, the end dword and the stored crc with its last.
+    // The verify kernel issues them only there (WAL verify +6.8 % against
+    // issuing them with every task, from a zero region when unused:
+    // profiles/r02s3w_*); the sealing kernel issues them with every task
+    // (2.5 % faster that way in the same A/B).  Loads written under branches:
+    // at 16 waves hipcc, short of VGPRs, copied such registers at the merge
+    // before their wait; the CFG audit run by build() fails on any such touch,
+    // and this build has none.
+    constexpr bool kSideAlways = !kVerify;
     const bool live = t.rb < n;
     const bool owned = live && ((vmeta >> 25) & 1u);
     const bool lastk = t.k + 1u == t.K;
+    if (kSideAlways || t.k == 0) fetch_desc(t.nrb);
     VP[sl] = vp;
     META[sl] = live ? vmeta : 0u;
     INIT[sl] = vinit;
-    HD[sl] = asm_load_u32(owned && t.k == 0 ? vp & ~3ull : zero);
-    ED[sl] = asm_load_u32(owned && lastk ? vp + vlen - 4u : zero);
-    if (kVerify) SC[sl] = asm_load_u32(owned && lastk ? (hdr ? vp - kLogCrcBack : vp + vlen) : zero);
+    if (kSideAlways || t.k == 0) HD[sl] = asm_load_u32(owned && t.k == 0 ? vp & ~3ull : zero);
+    if (kSideAlways || lastk) {
+      ED[sl] = asm_load_u32(owned && lastk ? vp + vlen - 4u : zero);
+      if (kVerify) SC[sl] = asm_load_u32(owned && lastk ? (hdr ? vp - kLogCrcBack : vp + vlen) : zero);
+    }
     // line min(k, kend - 1) of the lane's record (a finished lane re-reads its last)
     const uint32_t kl = live ? (t.k < vkend ? t.k : vkend - 1u) : 0u;
     asm_load_line(W[sl], (live ? vl : zero) + 128u * kl);
