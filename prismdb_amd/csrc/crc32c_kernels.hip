@@ -1952,11 +1952,6 @@ __device__ __forceinline__ void load_slice_tables(uint32_t* lds, const DeviceTab
   }
 }
 
-__device__ __forceinline__ u32x4 asm_load_x4(uint64_t addr) {
-  u32x4 r;
-  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(r) : "v"(addr));
-  return r;
-}
 // One 128-B line (lane kernel body): eight 16-B loads at immediate offsets.
 template <int J = 0>
 __device__ __forceinline__ void asm_load_line(u32x4 (&w)[8], uint64_t addr) {
@@ -1964,12 +1959,6 @@ __device__ __forceinline__ void asm_load_line(u32x4 (&w)[8], uint64_t addr) {
     asm volatile("global_load_dwordx4 %0, %1, off offset:%2" : "=v"(w[J]) : "v"(addr), "n"(16 * J));
     asm_load_line<J + 1>(w, addr);
   }
-}
-template <int kImm>
-__device__ __forceinline__ u32x4 asm_load_x4_at(uint64_t addr) {
-  u32x4 r;
-  asm volatile("global_load_dwordx4 %0, %1, off offset:%2" : "=v"(r) : "v"(addr), "n"(kImm));
-  return r;
 }
 __device__ __forceinline__ uint32_t asm_load_u32(uint64_t addr) {
   uint32_t r;
