@@ -63,6 +63,14 @@ def _declare(lib: ctypes.CDLL) -> None:
         "leveldb_crc32c_last_error": (ctypes.c_char_p, []),
         "prismdb_fill_synthetic": (ctypes.c_int, [vp, sz, u64, u64, vp]),
         "prismdb_crc32c_extend_portable": (u32, [u32, cp, sz]),
+        # test hooks (not in the public headers): path pinning
+        "prismdb_crc32c_force_generic": (None, [ctypes.c_int]),
+        "prismdb_crc32c_lane_mode": (None, [ctypes.c_int]),
+        "prismdb_crc32c_direct_max": (u64, [u64]),
+        "prismdb_crc32c_last_split": (ctypes.c_int, [vp]),
+        "prismdb_crc32c_direct_tickets": (u32, [u32]),
+        "prismdb_crc32c_direct_debug": (u32, [u32]),
+        "prismdb_crc32c_direct_stats": (ctypes.c_int, [vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

@@ -25,9 +25,9 @@ OBJDIR = os.path.join(ROOT, "build", "obj")
 LIB = os.path.join(LIBDIR, "libprismdb_crc32c.so")
 
 ARCH = os.environ.get("PRISMDB_OFFLOAD_ARCH", "gfx950")
-HIP_SOURCES = ["crc32c_kernels.hip", "crc32c_capi.hip", "crc32c_pipeline.hip", "synth.hip"]
+HIP_SOURCES = ["crc32c_kernels.hip", "crc32c_direct.hip", "crc32c_capi.hip", "crc32c_pipeline.hip", "synth.hip"]
 CXX_SOURCES = ["crc32c_host.cc", "sst.cc", "log_reader.cc"]
-HEADERS = ["crc32c_device.h", "crc32c_gf2.h"]
+HEADERS = ["crc32c_device.h", "crc32c_gf2.h", "crc32c_fold.h"]
 
 
 def _hipcc() -> str:

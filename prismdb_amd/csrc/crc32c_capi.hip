@@ -1,27 +1,26 @@
 // crc32c_capi.hip -- C ABI of the batch engine (include/prismdb_crc32c.h).
 //
 // Per-device context (tables in HBM, CU count, self-test) is created once with
-// std::call_once; after that every call is lock-free.  The long-span split
-// path needs a small workspace; it is cached per (thread, device, stream) so
-// concurrent callers on distinct streams never share one.
+// std::call_once; after that every call is lock-free.  The descriptor paths
+// need a workspace (ticket map, span records, split-path scratch); it is
+// cached per (thread, device, stream) so concurrent callers on distinct
+// streams never share one, grown stream-ordered (hipMallocAsync /
+// hipFreeAsync: no device-wide synchronisation), and released when the
+// thread exits or when the thread has used more than kMaxWorkspaces streams.
 #include <hip/hip_runtime.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 
+#include <atomic>
 #include <cstdio>
 #include <cstring>
-#include <map>
+#include <list>
 #include <mutex>
 #include <string>
 #include <utility>
 
 #include "../../include/prismdb_crc32c.h"
 #include "crc32c_device.h"
-
-#ifndef PRISMDB_SPAN_J0
-#define PRISMDB_SPAN_J0 0
-#endif
-#ifndef PRISMDB_SPAN_INJ0
-#define PRISMDB_SPAN_INJ0 0
-#endif
 #include "crc32c_gf2.h"
 
 namespace {
@@ -36,6 +35,8 @@ thread_local std::string t_last_error;
 // (read back only by the test hook prismdb_crc32c_last_split).
 thread_local const prismdb::dev::SplitCounters* t_last_counters = nullptr;
 thread_local hipStream_t t_last_stream = nullptr;
+thread_local bool t_last_direct = false;
+thread_local const uint32_t* t_last_stats = nullptr;
 
 int Fail(int code, const std::string& msg) {
   t_last_error = msg;
@@ -58,16 +59,19 @@ struct DeviceCtx {
 
 DeviceCtx g_ctx[kMaxDevices];
 
-// Test hook: route fixed-stride batches through the generic span kernel.
-bool g_force_generic = false;
-
-// Which descriptor batches go through the quad kernel first (spans of
-// <= kQuadMaxLen bytes; longer ones follow on the generic path):
-// 0 = log-record batches (PRISMDB_CRC32C_LOG_HEADER), 1 = all, -1 = none.
-#ifndef PRISMDB_QUAD_DEFAULT
-#define PRISMDB_QUAD_DEFAULT 0
-#endif
-int g_quad_mode = PRISMDB_QUAD_DEFAULT;
+// Test hooks (read on every call: atomics, relaxed).
+// Route fixed-stride batches through the generic span kernel.
+std::atomic<bool> g_force_generic{false};
+// Which planner-path descriptor batches go through the lane kernel first
+// (spans of kLaneMinLen..kLaneMaxLen bytes; the rest follow on the generic
+// path): 0 = log-record batches (PRISMDB_CRC32C_LOG_HEADER), 1 = all, -1 = none.
+std::atomic<int> g_lane_mode{0};
+// Descriptor batches of at most this many spans take the one-launch kernel.
+std::atomic<uint64_t> g_direct_max{prismdb::dev::kDirectMaxSpans};
+// The one-launch path's ticket capacity (tests shrink it to reach the
+// whole-span fallback) and its debug flags (DirectWs::dbg).
+std::atomic<uint32_t> g_direct_cap{prismdb::dev::kDirectTickets};
+std::atomic<uint32_t> g_direct_dbg{0};
 
 void BuildTables(DeviceTables* t) {
   namespace g = prismdb::gf2;
@@ -86,18 +90,26 @@ void BuildTables(DeviceTables* t) {
     const g::Op m = g::ShiftBytes((63ull - (uint64_t)l) * prismdb::dev::kSegment);
     for (int i = 0; i < 32; ++i) t->lane_seg[i][l] = m.col[i];
   }
+  // one-launch path: tickets of 2^lg chunks of 4 KiB
+  const g::Op c = g::ShiftBytes(4096u);
+  for (int i = 0; i < 32; ++i) t->shift_chunk[i] = c.col[i];
+  for (int lg = 0; lg < 4; ++lg) {
+    const uint64_t tb = 4096ull << lg;
+    const g::Op m64 = g::ShiftBytes(64ull * tb);
+    for (int i = 0; i < 32; ++i) t->tick64[lg][i] = m64.col[i];
+    for (int l = 0; l < 64; ++l) {
+      const g::Op m = g::ShiftBytes((63ull - (uint64_t)l) * tb);
+      for (int i = 0; i < 32; ++i) t->tick_lane[lg][i][l] = m.col[i];
+    }
+  }
 }
 
-int RunBatch(DeviceCtx& ctx, const SpanBatch& base_args, bool desc, bool verify, hipStream_t s);
+int RunBatch(DeviceCtx& ctx, const SpanBatch& base_args, bool desc, bool verify, hipStream_t s, int route);
 
 // Device known-answer self-test (util/crc32c.cc:269-273 vector, plus a 4 KiB
-// block and a > kLongSpan span checked against the host Extend).
+// block and a > kLongSpan span checked against the host Extend), through both
+// descriptor paths: the one-launch kernel (route 1) and the planner (route 2).
 int SelfTest(DeviceCtx& ctx) {
-#ifdef PRISMDB_MEASURE_ONLY
-  // measurement-only variant builds (tools/variants.py) that knowingly break
-  // results on some geometries skip the self-test; the product never defines it
-  return 0;
-#endif
   const size_t kBig = prismdb::dev::kLongSpan + 3 * prismdb::dev::kSegment + 77;
   const size_t bytes = 64 + 4096 + kBig;
   unsigned char* h = new unsigned char[bytes];
@@ -138,26 +150,30 @@ int SelfTest(DeviceCtx& ctx) {
   a.len = d_len;
   a.n = 3;
   a.out = d_out;
-  int rc = RunBatch(ctx, a, true, false, nullptr);
-  uint32_t got[3] = {0, 0, 0};
-  if (rc == 0) {
-    e = hipStreamSynchronize(nullptr);
-    if (e != hipSuccess) rc = FailHip(e, "self-test sync");
-  }
-  if (rc == 0) {
-    e = hipMemcpy(got, d_out, sizeof(got), hipMemcpyDeviceToHost);
-    if (e != hipSuccess) rc = FailHip(e, "self-test download");
+  int rc = 0;
+  for (int route = 1; route <= 2 && rc == 0; ++route) {
+    uint32_t got[3] = {0, 0, 0};
+    e = hipMemset(d_out, 0, sizeof(got));
+    if (e != hipSuccess) rc = FailHip(e, "self-test memset");
+    if (rc == 0) rc = RunBatch(ctx, a, true, false, nullptr, route);
+    if (rc == 0) {
+      e = hipStreamSynchronize(nullptr);
+      if (e != hipSuccess) rc = FailHip(e, "self-test sync");
+    }
+    if (rc == 0) {
+      e = hipMemcpy(got, d_out, sizeof(got), hipMemcpyDeviceToHost);
+      if (e != hipSuccess) rc = FailHip(e, "self-test download");
+    }
+    if (rc == 0 && (got[0] != want[0] || got[1] != want[1] || got[2] != want[2])) {
+      char buf[200];
+      std::snprintf(buf, sizeof(buf), "device self-test (%s path): got %08x %08x %08x want %08x %08x %08x",
+                    route == 1 ? "one-launch" : "planner", got[0], got[1], got[2], want[0], want[1], want[2]);
+      rc = Fail(PRISMDB_CRC32C_ESELFTEST, buf);
+    }
   }
   hipFree(d);
   delete[] h;
-  if (rc != 0) return rc;
-  if (got[0] != want[0] || got[1] != want[1] || got[2] != want[2]) {
-    char buf[200];
-    std::snprintf(buf, sizeof(buf), "device self-test: got %08x %08x %08x want %08x %08x %08x", got[0],
-                  got[1], got[2], want[0], want[1], want[2]);
-    return Fail(PRISMDB_CRC32C_ESELFTEST, buf);
-  }
-  return 0;
+  return rc;
 }
 
 void InitDevice(DeviceCtx& ctx, int device) {
@@ -178,10 +194,8 @@ void InitDevice(DeviceCtx& ctx, int device) {
     ctx.error = t_last_error;
     return;
   }
-#if PRISMDB_SPAN_J0 == 0 && !PRISMDB_SPAN_INJ0  // measurement-only builds compute wrong CRCs on purpose
   ctx.status = SelfTest(ctx);
   if (ctx.status != 0) ctx.error = t_last_error;
-#endif
 }
 
 int GetCtx(DeviceCtx** out) {
@@ -196,92 +210,161 @@ int GetCtx(DeviceCtx** out) {
   return 0;
 }
 
-// ---- generic-path workspace, per (thread, device, stream) ----
-// Fixed part: split-path counters, segment records/results, long-span list,
-// planner block sums.  Growing part, sized for the largest batch seen (the
-// first call with a larger batch synchronises the stream and reallocates): per
-// span a 16-byte record and a 4-byte task count, plus the slice starts.
+// ---- workspaces, per (thread, device, stream) ----
+// Fixed part, allocated once: split-path counters, segment records and
+// results, the long-span table, the planner's block sums.  Growing parts,
+// sized for the largest batch seen: the span records (16 B + a 4-byte task
+// count per span, plus the slice starts), the lane path's list (9 B per span)
+// and the one-launch path's ticket workspace (allocated on its first use).
+// Growth frees the old block on the stream, behind the work still reading
+// it (hipFreeAsync), so one thread's growth never stalls other streams.
 struct Workspace {
+  int device = -1;
+  hipStream_t stream = nullptr;
   void* mem = nullptr;
   char* grow = nullptr;
   size_t cap_rec = 0;
-  char* qgrow = nullptr;  // quad path: long-span list and its results (9 B per span), run flags
+  char* qgrow = nullptr;
   size_t cap_q = 0;
+  char* direct = nullptr;  // word, done | ticket map | partials | per-span counters
+  uint32_t gen = 0;
   SplitWs ws{};
 };
 
+// A thread that has used more streams than this evicts its least recently
+// used workspace (after synchronising that device: rare by construction).
+constexpr size_t kMaxWorkspaces = 8;
+
+// Every block of w, after the device has finished all work (callers
+// synchronise): stream-ordered frees on the null stream.
+void ReleaseWorkspace(Workspace& w) {
+  if (w.mem) (void)hipFree(w.mem);
+  if (w.grow) (void)hipFreeAsync(w.grow, nullptr);
+  if (w.qgrow) (void)hipFreeAsync(w.qgrow, nullptr);
+  if (w.direct) (void)hipFreeAsync(w.direct, nullptr);
+  (void)hipStreamSynchronize(nullptr);
+  w = Workspace{};
+}
+
+void SyncAndRelease(Workspace& w) {
+  if (t_last_counters == w.ws.counters) t_last_counters = nullptr;
+  if (w.direct != nullptr && t_last_stats == reinterpret_cast<const uint32_t*>(w.direct + 16)) t_last_stats = nullptr;
+  int cur = 0;
+  (void)hipGetDevice(&cur);
+  if (w.device != cur) (void)hipSetDevice(w.device);
+  (void)hipDeviceSynchronize();
+  ReleaseWorkspace(w);
+  if (w.device != cur) (void)hipSetDevice(cur);
+}
+
+struct WorkspaceCache {
+  std::list<Workspace> lru;  // most recently used first
+  ~WorkspaceCache() {
+    // A worker thread gives its device memory back when it exits.  The main
+    // thread's thread-local destructors run inside exit(), where the HIP
+    // runtime (or a profiler wrapped around it) may be tearing down already:
+    // its workspaces are left to the OS (as the host pipeline's rings are).
+    if (syscall(SYS_gettid) == getpid()) return;
+    for (Workspace& w : lru) SyncAndRelease(w);
+  }
+};
+
 // Slice starts needed for n spans: nslices + 1 <= n/2 + 32 * streams + 2
-// (crc32c_slice_scan_kernel: tau = 64 gives <= n/2 + 1 slices of <= 32-task
-// spans; a smaller tau keeps tau > T / (32 * streams)).
-#ifndef PRISMDB_SLICES_PER_STREAM
-#define PRISMDB_SLICES_PER_STREAM 16
-#endif
+// (crc32c_slice_scan_kernel: K = m S slices with m <= kSlicesPerStream or
+// enough slices to keep <= 63 tasks each).
 size_t SliceCap(size_t n, uint32_t streams) {
-  return n / 2 + 2 * (size_t)PRISMDB_SLICES_PER_STREAM * streams + 4;
+  return n / 2 + 2 * (size_t)prismdb::dev::kSlicesPerStream * streams + 4;
 }
 
 constexpr uint64_t kCapSeg = 1u << 20;   // 1 Mi segments = 32 GiB of long spans per call
 constexpr uint32_t kCapLong = 1u << 18;
 
-int GetWorkspace(hipStream_t s, size_t nspans, uint32_t streams, bool quad, SplitWs* out) {
-  thread_local std::map<std::pair<int, hipStream_t>, Workspace> cache;
+Workspace* FindWorkspace(hipStream_t s, int& rc) {
+  thread_local WorkspaceCache cache;
   int device = 0;
-  hipGetDevice(&device);
-  Workspace& w = cache[{device, s}];
-  if (w.mem == nullptr) {
-    const size_t bytes = 256 + kCapSeg * (16 + 4) + (size_t)kCapLong * (8 + 8 + 4) +
-                         (size_t)prismdb::dev::kMaxPlanBlocks * 8;
-    hipError_t e = hipMalloc(&w.mem, bytes);
-    if (e != hipSuccess) {
-      w.mem = nullptr;
-      return FailHip(e, "workspace hipMalloc");
-    }
-    char* p = static_cast<char*>(w.mem);
-    w.ws.counters = reinterpret_cast<SplitCounters*>(p);
-    p += 256;
-    w.ws.seg_rec = reinterpret_cast<prismdb::dev::SpanRec*>(p);
-    p += kCapSeg * 16;
-    w.ws.long_span = reinterpret_cast<uint64_t*>(p);
-    p += (size_t)kCapLong * 8;
-    w.ws.long_first = reinterpret_cast<uint64_t*>(p);
-    p += (size_t)kCapLong * 8;
-    w.ws.seg_out = reinterpret_cast<uint32_t*>(p);
-    p += kCapSeg * 4;
-    w.ws.long_nseg = reinterpret_cast<uint32_t*>(p);
-    p += (size_t)kCapLong * 4;
-    w.ws.bsum = reinterpret_cast<uint64_t*>(p);
-    w.ws.cap_seg = kCapSeg;
-    w.ws.cap_long = kCapLong;
+  hipError_t e = hipGetDevice(&device);
+  if (e != hipSuccess) {
+    rc = FailHip(e, "hipGetDevice");
+    return nullptr;
   }
-  if (w.cap_rec < nspans) {
-    if (w.grow != nullptr) {
-      hipStreamSynchronize(s);  // earlier batches on this stream may still read it
-      hipFree(w.grow);
-      w.grow = nullptr;
-      w.cap_rec = 0;
+  auto& lru = cache.lru;
+  for (auto it = lru.begin(); it != lru.end(); ++it) {
+    if (it->device == device && it->stream == s) {
+      if (it != lru.begin()) lru.splice(lru.begin(), lru, it);
+      rc = 0;
+      return &lru.front();
     }
+  }
+  if (lru.size() >= kMaxWorkspaces) {
+    SyncAndRelease(lru.back());
+    lru.pop_back();
+  }
+  lru.emplace_front();
+  Workspace& w = lru.front();
+  w.device = device;
+  w.stream = s;
+  const size_t bytes = 256 + kCapSeg * (16 + 4) + (size_t)kCapLong * (8 + 8 + 4) +
+                       (size_t)prismdb::dev::kMaxPlanBlocks * 8;
+  e = hipMalloc(&w.mem, bytes);
+  if (e != hipSuccess) {
+    lru.pop_front();
+    rc = FailHip(e, "workspace hipMalloc");
+    return nullptr;
+  }
+  char* p = static_cast<char*>(w.mem);
+  w.ws.counters = reinterpret_cast<SplitCounters*>(p);
+  p += 256;
+  w.ws.seg_rec = reinterpret_cast<prismdb::dev::SpanRec*>(p);
+  p += kCapSeg * 16;
+  w.ws.long_span = reinterpret_cast<uint64_t*>(p);
+  p += (size_t)kCapLong * 8;
+  w.ws.long_first = reinterpret_cast<uint64_t*>(p);
+  p += (size_t)kCapLong * 8;
+  w.ws.seg_out = reinterpret_cast<uint32_t*>(p);
+  p += kCapSeg * 4;
+  w.ws.long_nseg = reinterpret_cast<uint32_t*>(p);
+  p += (size_t)kCapLong * 4;
+  w.ws.bsum = reinterpret_cast<uint64_t*>(p);
+  w.ws.cap_seg = kCapSeg;
+  w.ws.cap_long = kCapLong;
+  rc = 0;
+  return &w;
+}
+
+// Replace *blk (size irrelevant) by a fresh block of `bytes` on stream s; the
+// old one is freed behind the work already enqueued on s.
+int GrowBlock(char** blk, size_t bytes, hipStream_t s, const char* what) {
+  if (*blk != nullptr) {
+    hipError_t e = hipFreeAsync(*blk, s);
+    *blk = nullptr;
+    if (e != hipSuccess) return FailHip(e, what);
+  }
+  hipError_t e = hipMallocAsync(reinterpret_cast<void**>(blk), bytes, s);
+  if (e != hipSuccess) {
+    *blk = nullptr;
+    return FailHip(e, what);
+  }
+  return 0;
+}
+
+int PlannerWorkspace(Workspace& w, hipStream_t s, size_t nspans, uint32_t streams, bool lane, SplitWs* out) {
+  if (w.cap_rec < nspans) {
     const size_t cap = nspans < 4096 ? 4096 : nspans + nspans / 4;
     const size_t bytes = cap * (16 + 4) + SliceCap(cap, streams) * 8 + 16;
-    hipError_t e = hipMalloc(reinterpret_cast<void**>(&w.grow), bytes);
-    if (e != hipSuccess) return FailHip(e, "span record workspace hipMalloc");
+    w.cap_rec = 0;
+    if (int rc = GrowBlock(&w.grow, bytes, s, "span record workspace")) return rc;
     w.cap_rec = cap;
   }
-  if (quad && w.cap_q < nspans) {
-    if (w.qgrow != nullptr) {
-      hipStreamSynchronize(s);
-      hipFree(w.qgrow);
-      w.qgrow = nullptr;
-      w.cap_q = 0;
-    }
+  if (lane && w.cap_q < nspans) {
     const size_t cap = nspans < 4096 ? 4096 : nspans + nspans / 4;
-    hipError_t e = hipMalloc(reinterpret_cast<void**>(&w.qgrow), cap * 9 + cap / 64 + 1024);
-    if (e != hipSuccess) return FailHip(e, "quad list workspace hipMalloc");
+    w.cap_q = 0;
+    if (int rc = GrowBlock(&w.qgrow, cap * 9 + cap / 64 + 1024, s, "lane list workspace")) return rc;
     w.cap_q = cap;
   }
-  w.ws.list = quad ? reinterpret_cast<uint32_t*>(w.qgrow) : nullptr;
-  w.ws.qout = quad ? reinterpret_cast<uint32_t*>(w.qgrow + w.cap_q * 4) : nullptr;
-  w.ws.qmm = quad ? reinterpret_cast<uint8_t*>(w.qgrow + w.cap_q * 8) : nullptr;
-  w.ws.qrun = quad ? reinterpret_cast<uint8_t*>(w.qgrow + w.cap_q * 9) : nullptr;
+  w.ws.list = lane ? reinterpret_cast<uint32_t*>(w.qgrow) : nullptr;
+  w.ws.qout = lane ? reinterpret_cast<uint32_t*>(w.qgrow + w.cap_q * 4) : nullptr;
+  w.ws.qmm = lane ? reinterpret_cast<uint8_t*>(w.qgrow + w.cap_q * 8) : nullptr;
+  w.ws.qrun = lane ? reinterpret_cast<uint8_t*>(w.qgrow + w.cap_q * 9) : nullptr;
   w.ws.rec = reinterpret_cast<prismdb::dev::SpanRec*>(w.grow);
   w.ws.slice_start = reinterpret_cast<uint64_t*>(w.grow + w.cap_rec * 16);
   w.ws.cnt = reinterpret_cast<uint32_t*>(w.grow + w.cap_rec * 16 + SliceCap(w.cap_rec, streams) * 8);
@@ -295,10 +378,39 @@ int GetWorkspace(hipStream_t s, size_t nspans, uint32_t streams, bool quad, Spli
   return 0;
 }
 
-// Launch sequence.  Fast path: one kernel.  Generic path:
-// plan (span records, long spans cut into segments) -> span pass (long spans
-// skipped) -> segment pass -> combine.
-int RunBatch(DeviceCtx& ctx, const SpanBatch& base_args, bool desc, bool verify, hipStream_t s) {
+// The one-launch path's workspace: counters (zero between calls: the kernel's
+// last group resets them), the ticket map (entries carry the call's gen), the
+// partial registers and the per-span ticket counters (zero between calls).
+int DirectWorkspace(Workspace& w, hipStream_t s, prismdb::dev::DirectWs* out) {
+  namespace d = prismdb::dev;
+  const size_t cap = d::kDirectTickets;
+  const size_t bytes = 256 + cap * (16 + 4 + 4);
+  if (w.direct == nullptr) {
+    if (int rc = GrowBlock(&w.direct, bytes, s, "ticket workspace")) return rc;
+    hipError_t e = hipMemsetAsync(w.direct, 0, bytes, s);
+    if (e != hipSuccess) return FailHip(e, "ticket workspace memset");
+  }
+  char* p = w.direct;
+  out->word = reinterpret_cast<unsigned long long*>(p);
+  out->done = reinterpret_cast<uint32_t*>(p + 8);
+  out->stats = reinterpret_cast<uint32_t*>(p + 16);
+  out->tmap = reinterpret_cast<uint32_t*>(p + 256);
+  out->part = reinterpret_cast<uint32_t*>(p + 256 + cap * 16);
+  out->cdone = reinterpret_cast<uint32_t*>(p + 256 + cap * 20);
+  out->cap = g_direct_cap.load(std::memory_order_relaxed);
+  out->dbg = g_direct_dbg.load(std::memory_order_relaxed);
+  out->gen = ++w.gen == 0 ? ++w.gen : w.gen;  // 0 is the zeroed map's
+  return 0;
+}
+
+enum Route { kRouteAuto = 0, kRouteDirect = 1, kRoutePlanner = 2 };
+
+// Launch sequence.  Fixed stride, aligned, <= 4 KiB: one kernel.  Descriptor
+// batches of <= g_direct_max spans: one kernel (crc32c_direct.hip).  The
+// rest: plan (span records, long spans cut into segments) -> span pass (long
+// spans skipped) -> segment pass -> combine, with the lane kernel and its
+// list in front for log-record batches.
+int RunBatch(DeviceCtx& ctx, const SpanBatch& base_args, bool desc, bool verify, hipStream_t s, int route) {
   SpanBatch a = base_args;
   a.tabs = ctx.tabs;
   a.role = prismdb::dev::kRoleSpans;
@@ -309,9 +421,25 @@ int RunBatch(DeviceCtx& ctx, const SpanBatch& base_args, bool desc, bool verify,
   if (!desc && (verify || a.out != nullptr) && (!verify || (a.len_c & 255u) != 0) &&
       (a.flags & (prismdb::dev::kFlagWriteTrailer | prismdb::dev::kFlagLogHeader)) == 0 &&
       a.len_c >= 4 && a.len_c <= max_len && (a.len_c & 3u) == 0 &&
-      (a.stride & 3u) == 0 && (reinterpret_cast<uintptr_t>(a.base) & 3u) == 0 && !g_force_generic) {
+      (a.stride & 3u) == 0 && (reinterpret_cast<uintptr_t>(a.base) & 3u) == 0 &&
+      !g_force_generic.load(std::memory_order_relaxed)) {
     hipError_t e = prismdb::dev::launch_fixed(a, verify, ctx.cus, s);
     return e == hipSuccess ? 0 : FailHip(e, "fixed kernel launch");
+  }
+  int rc = 0;
+  Workspace* w = FindWorkspace(s, rc);
+  if (w == nullptr) return rc;
+  const bool direct = desc && (route == kRouteDirect ||
+                               (route == kRouteAuto && a.n <= g_direct_max.load(std::memory_order_relaxed)));
+  if (direct && a.n <= prismdb::dev::kDirectMaxSpans &&
+      a.n <= 64ull * (uint64_t)ctx.cus * (prismdb::dev::kDirectThreads / 64)) {
+    prismdb::dev::DirectWs d{};
+    if ((rc = DirectWorkspace(*w, s, &d)) != 0) return rc;
+    t_last_direct = true;
+    t_last_stats = d.stats;
+    t_last_stream = s;
+    hipError_t e = prismdb::dev::launch_direct(a, verify, ctx.cus, d, s);
+    return e == hipSuccess ? 0 : FailHip(e, "direct kernel launch");
   }
   // The span kernel indexes records with 32 bits: cut larger batches.
   if (a.n > prismdb::dev::kMaxGenericSpans) {
@@ -327,29 +455,29 @@ int RunBatch(DeviceCtx& ctx, const SpanBatch& base_args, bool desc, bool verify,
       }
       if (p.out != nullptr) p.out += i;
       if (p.mismatch != nullptr) p.mismatch += i;
-      const int rc = RunBatch(ctx, p, desc, verify, s);
-      if (rc != 0) return rc;
+      if ((rc = RunBatch(ctx, p, desc, verify, s, kRoutePlanner)) != 0) return rc;
     }
     return 0;
   }
   SplitWs ws{};
   // The span kernel's record streams: two per wave of its persistent grid.
   const uint32_t streams = 2u * (uint32_t)ctx.cus * prismdb::dev::kWavesPerGroup;
-  // Short spans first, four per wave (crc32c_quad_kernel); the generic path
-  // below then runs over the list of the longer ones only.
-  const bool quad = desc && (g_quad_mode > 0 || (g_quad_mode == 0 && (a.flags & prismdb::dev::kFlagLogHeader)));
-  int rc = GetWorkspace(s, a.n, streams, quad, &ws);
-  if (rc != 0) return rc;
+  // Short spans first, one per lane (crc32c_lane_kernel); the generic path
+  // below then runs over the list of the others only.
+  const int lane_mode = g_lane_mode.load(std::memory_order_relaxed);
+  const bool lane = desc && (lane_mode > 0 || (lane_mode == 0 && (a.flags & prismdb::dev::kFlagLogHeader)));
+  if ((rc = PlannerWorkspace(*w, s, a.n, streams, lane, &ws)) != 0) return rc;
   hipError_t e = hipMemsetAsync(ws.counters, 0, sizeof(SplitCounters), s);
   if (e != hipSuccess) return FailHip(e, "hipMemsetAsync");
   t_last_counters = ws.counters;
   t_last_stream = s;
+  t_last_direct = false;
   uint32_t* const caller_out = a.out;
   uint8_t* const caller_mm = a.mismatch;
-  if (quad) {
+  if (lane) {
     a.qrun = ws.qrun;
-    e = prismdb::dev::launch_quad(a, verify, ctx.cus, ws, s);
-    if (e != hipSuccess) return FailHip(e, "quad kernel launch");
+    e = prismdb::dev::launch_lane(a, verify, ctx.cus, ws, s);
+    if (e != hipSuccess) return FailHip(e, "lane kernel launch");
     a.idx = ws.list;
     a.n_dev = &ws.counters->nlist;
     if (a.out != nullptr) a.out = ws.qout;
@@ -374,7 +502,7 @@ int RunBatch(DeviceCtx& ctx, const SpanBatch& base_args, bool desc, bool verify,
   // Large batches of one-task records take the pair-run kernel (its two
   // streams read adjacent spans); it is launched next to the general one,
   // and the one whose schedule the scan did not pick leaves at once.
-  a.pair_kernel = PRISMDB_SPAN_PAIR_RUNS && a.slice_start != nullptr && a.n >= prismdb::dev::kPairMinSpans &&
+  a.pair_kernel = a.slice_start != nullptr && a.n >= prismdb::dev::kPairMinSpans && !lane &&
                           !(a.flags & prismdb::dev::kFlagLogHeader)
                       ? 1u
                       : 0u;
@@ -394,7 +522,7 @@ int RunBatch(DeviceCtx& ctx, const SpanBatch& base_args, bool desc, bool verify,
   if (e != hipSuccess) return FailHip(e, "segment kernel launch");
   e = prismdb::dev::launch_combine(a, desc, verify, ws, s);
   if (e != hipSuccess) return FailHip(e, "combine kernel launch");
-  if (quad) {
+  if (lane) {
     SpanBatch back = a;
     back.out = caller_out;
     back.mismatch = caller_mm;
@@ -448,7 +576,7 @@ int leveldb_crc32c_batch_fixed(const void* dev_base, size_t stride, size_t len, 
   a.out = dev_out;
   a.mismatch = dev_mismatch;
   a.flags = flags;
-  return RunBatch(*ctx, a, false, dev_mismatch != nullptr, static_cast<hipStream_t>(stream));
+  return RunBatch(*ctx, a, false, dev_mismatch != nullptr, static_cast<hipStream_t>(stream), 0);
 }
 
 int leveldb_crc32c_batch(const void* dev_base, const uint64_t* dev_off, const uint32_t* dev_len,
@@ -473,24 +601,57 @@ int leveldb_crc32c_batch(const void* dev_base, const uint64_t* dev_off, const ui
   a.out = dev_out;
   a.mismatch = dev_mismatch;
   a.flags = flags;
-  return RunBatch(*ctx, a, true, dev_mismatch != nullptr, static_cast<hipStream_t>(stream));
+  return RunBatch(*ctx, a, true, dev_mismatch != nullptr, static_cast<hipStream_t>(stream), 0);
 }
 
 const char* leveldb_crc32c_last_error(void) { return t_last_error.c_str(); }
 
-// Not in the public header: lets the parity tests pin the generic kernel too.
-void prismdb_crc32c_force_generic(int on) { g_force_generic = on != 0; }
+// Test hooks, not in the public header (the parity tests and the A/B harness
+// pin each path with them):
+// fixed-stride batches through the generic span kernel too;
+void prismdb_crc32c_force_generic(int on) { g_force_generic.store(on != 0, std::memory_order_relaxed); }
 
-// Not in the public header: which descriptor batches take the quad kernel
-// (0 = log-record batches, the default; 1 = every batch; -1 = none), so the
-// parity tests and the A/B harness can pin either path.
-void prismdb_crc32c_quad_mode(int mode) { g_quad_mode = mode > 0 ? 1 : (mode < 0 ? -1 : 0); }
+// which planner-path descriptor batches take the lane kernel first (0 =
+// log-record batches, the default; 1 = every batch; -1 = none);
+void prismdb_crc32c_lane_mode(int mode) {
+  g_lane_mode.store(mode > 0 ? 1 : (mode < 0 ? -1 : 0), std::memory_order_relaxed);
+}
 
-// Not in the public header: the split counters of the calling thread's last
-// descriptor batch {long spans, segments, overflow flag, spans listed by the
-// quad kernel}, after waiting for its stream, so the tests can tell which
-// path a batch took.  Returns 0, or -1 if the thread has run no such batch.
+// descriptor batches of at most this many spans take the one-launch kernel
+// (clamped to kDirectMaxSpans; 0: none do); returns the previous value.
+uint64_t prismdb_crc32c_direct_max(uint64_t n) {
+  if (n > prismdb::dev::kDirectMaxSpans) n = prismdb::dev::kDirectMaxSpans;
+  return g_direct_max.exchange(n, std::memory_order_relaxed);
+}
+
+// the one-launch path's ticket capacity (clamped to 1..kDirectTickets) and
+// debug flags (bit 0: delay the pushes, see DirectWs::dbg); return the old values.
+uint32_t prismdb_crc32c_direct_tickets(uint32_t cap) {
+  if (cap < 1u) cap = 1u;
+  if (cap > prismdb::dev::kDirectTickets) cap = prismdb::dev::kDirectTickets;
+  return g_direct_cap.exchange(cap, std::memory_order_relaxed);
+}
+uint32_t prismdb_crc32c_direct_debug(uint32_t flags) { return g_direct_dbg.exchange(flags, std::memory_order_relaxed); }
+
+// the cumulative one-launch counters of the workspace of the calling thread's
+// last one-launch batch {tickets adopted, spans folded whole, tickets claimed
+// early, tickets claimed late}, after waiting for its stream.  0, or -1.
+int prismdb_crc32c_direct_stats(uint64_t out[4]) {
+  if (t_last_stats == nullptr) return -1;
+  uint32_t c[4] = {0, 0, 0, 0};
+  hipError_t e = hipStreamSynchronize(t_last_stream);
+  if (e == hipSuccess) e = hipMemcpy(c, t_last_stats, sizeof(c), hipMemcpyDeviceToHost);
+  if (e != hipSuccess) return FailHip(e, "prismdb_crc32c_direct_stats");
+  for (int i = 0; i < 4; ++i) out[i] = c[i];
+  return 0;
+}
+
+// the split counters of the calling thread's last planner-path descriptor
+// batch {long spans, segments, overflow flag, spans listed by the lane
+// kernel}, after waiting for its stream.  Returns 0; -1 if the thread has run
+// no such batch; -2 if its last descriptor batch took the one-launch path.
 int prismdb_crc32c_last_split(uint64_t out[4]) {
+  if (t_last_direct) return -2;
   if (t_last_counters == nullptr) return -1;
   prismdb::dev::SplitCounters c{};
   hipError_t e = hipStreamSynchronize(t_last_stream);

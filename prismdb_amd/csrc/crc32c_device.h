@@ -23,11 +23,8 @@ constexpr uint32_t kChunkWords = kRounds * kWave;  // 1024 words = 4 KiB per chu
 // Log-record span kernel chunk.  8 rounds (2 KiB) would make a ~1 KB record one
 // task of 9 loads, but hipcc then copies the ring's in-flight registers
 // (tools/check_inflight.py: 792 sites), so it stays at 16.
-#ifndef PRISMDB_ROUNDS_LOG
-#define PRISMDB_ROUNDS_LOG 16
-#endif
-constexpr int kRoundsLog = PRISMDB_ROUNDS_LOG;
-constexpr uint32_t kLgChunkWordsLog = kRoundsLog == 8 ? 9u : 10u;
+constexpr int kRoundsLog = 16;
+constexpr uint32_t kLgChunkWordsLog = 10u;
 constexpr uint32_t kStrideBytes = 4u * kWave;      // 256 B between a lane's words
 constexpr int kCopies = 32;                        // LDS table replication (bank = lane % 32)
 constexpr int kTabWords = 4 * 256 * kCopies;       // 128 KiB of LDS: stride tables
@@ -47,28 +44,20 @@ struct DeviceTables {
   uint32_t shift_seg64[32];   // column i of M^64
   uint32_t lane_seg[32][64];  // [i][l] = column i of M^(63-l): lane l's final shift
   uint32_t slice4[4][256];    // slice4[k][b] = shift_4(b << 8k): one record per lane (lane kernel)
-  // 64 KiB of zeros: the quad kernel's loads of lanes without a record to
-  // read land here, 256 B per wave (wave % 256) -- one shared line was an L2
-  // hotspot when whole tasks are left to the generic path
+  // One-launch path (crc32c_direct.hip): a long span's tickets of g = 2^lg
+  // chunks (lg 0..3) are combined with M = shift_{4 KiB * g}:
+  uint32_t tick64[4][32];         // [lg][i] = column i of M^64
+  uint32_t tick_lane[4][32][64];  // [lg][i][l] = column i of M^(63-l): lane l's final shift
+  uint32_t shift_chunk[32];       // column i of shift_{4 KiB} (tests; M for lg 0)
+  // 64 KiB of zeros: the lane kernel's loads of lanes without a record to
+  // read land here, 2 KiB per wave (wave % 32) -- one shared line was an L2
+  // hotspot when whole runs are left to the generic path
   uint32_t zero[kZeroWords];
 };
 
-// Short-record ("quad") kernel: spans of len <= kQuadMaxLen, four per wave,
-// each on one 16-lane DPP row with four 256-B-stride sub-streams per lane
-// (crc32c_kernels.hip).  A frame is kQuadRounds rounds of 64 words.
-constexpr int kQuadRounds = 5;
-constexpr uint32_t kQuadWords = 64u * kQuadRounds;   // 320 body words
-constexpr uint32_t kQuadMaxLen = 4u * kQuadWords;    // len <= 1280 B => <= 320 body words
-// A record's body-address arithmetic reaches kQuadBack bytes below its body
-// (unsigned, 32-bit offsets from the task's window base).
-constexpr uint32_t kQuadBack = kQuadMaxLen;
-
 // Lane kernel (log-record batches): one record per lane, 128-B tasks of eight
 // 16-B loads; records of kLaneMinLen..kLaneMaxLen bytes (the rest take the
-// generic path through the long-span list, as with the quad kernel).
-#ifndef PRISMDB_LANE_KERNEL
-#define PRISMDB_LANE_KERNEL 1
-#endif
+// generic path through the long-span list).
 constexpr uint32_t kLaneMinLen = 8u;  // >= 3 head bytes + one body word
 constexpr uint32_t kLaneMaxLen = 1280u;
 __host__ __device__ constexpr bool lane_owns(uint32_t len) { return len >= kLaneMinLen && len <= kLaneMaxLen; }
@@ -103,18 +92,15 @@ struct SpanBatch {
   const unsigned long long* nslices_dev;
   uint32_t chunk_lg;  // planner: log2(chunk words) of the kernel that consumes the span records
   // nullable: record i of this batch is span idx[i] of the caller's
-  // descriptors and results (the generic path behind the quad kernel runs
-  // over the list of spans too long for it; n_dev holds the list length)
+  // descriptors and results (the generic path behind the lane kernel runs
+  // over the list of spans it does not own; n_dev holds the list length)
   const uint32_t* idx;
-  const uint8_t* qrun;  // quad kernel: runs it owns a span of (crc32c_long_list_kernel)
+  const uint8_t* qrun;  // lane kernel: runs it owns a span of (crc32c_long_list_kernel)
   // Span role: the pair-run span kernel is launched too (it takes the batch
   // when the scan finds every record one task; the general kernel then leaves).
   uint32_t pair_kernel;
 };
 
-#ifndef PRISMDB_SPAN_PAIR_RUNS  // launch the pair-run span kernel for batches of >= kPairMinSpans spans
-#define PRISMDB_SPAN_PAIR_RUNS 1
-#endif
 // Below this many spans the pair-run kernel's extra launch (~5 us) costs more
 // than its 3.5 % gains (break-even near 140 us of data, ~250 K spans of 4 KiB).
 constexpr uint64_t kPairMinSpans = 1ull << 18;
@@ -124,9 +110,8 @@ struct SplitCounters {
   uint32_t nlong;
   uint32_t overflow;
   unsigned long long tasks;    // chunk tasks of the span pass (long spans count 1)
-  unsigned long long nslices;  // slices of 2^lg_tau tasks
-  uint32_t lg_tau;
-  unsigned long long nlist;             // spans the quad kernel leaves to the generic path
+  unsigned long long nslices;  // task-balanced slices (0: every record one task, runs instead)
+  unsigned long long nlist;             // spans the lane kernel leaves to the generic path
   unsigned long long slice_q, slice_r;  // exact slices: q = T / K, r = T % K
 };
 
@@ -147,14 +132,38 @@ struct SplitWs {
   uint64_t tile;          // records per planner block
   uint32_t nblocks;       // planner blocks (<= kMaxPlanBlocks)
   uint32_t nstreams;      // span-kernel record streams (2 per wave)
-  uint32_t* list;         // quad path: indices of the spans longer than kQuadMaxLen
-  uint32_t* qout;         // quad path: generic-path results of the listed spans (list order)
+  uint32_t* list;         // lane path: indices of the spans the lane kernel does not own
+  uint32_t* qout;         // lane path: generic-path results of the listed spans (list order)
   uint8_t* qmm;
-  uint8_t* qrun;          // quad path: per run of 64 spans, 1 if the quad kernel owns one of them
+  uint8_t* qrun;          // lane path: per run of 64 spans, 1 if the lane kernel owns one of them
                           // (read a dword at a time: the workspace has slack around it)
 };
 
+// One-launch path for descriptor batches of <= kDirectMaxSpans spans
+// (crc32c_direct.hip): one kernel, no planner, no memset.  Spans of one chunk
+// (body <= 4 KiB) are dealt to the waves in static runs; longer spans are cut
+// into tickets of 2^lg chunks that any wave may claim, and the wave that
+// finishes a span's last ticket combines the partial registers.
+constexpr uint64_t kDirectMaxSpans = 1ull << 17;
+constexpr int kDirectThreads = 512;  // per group, one group per CU: a wave's static run is <= 64 spans
+                                     // while n <= 64 * 8 * CUs (host-checked)
+constexpr uint32_t kDirectTickets = 1u << 20;  // ticket workspace (beyond it: whole spans, one wave each)
+constexpr uint32_t kNullSpan = 0xFFFFFFFFu;
+
+struct DirectWs {
+  unsigned long long* word;  // supply << 32 | claimed: tickets pushed / tickets taken
+  uint32_t* done;            // groups finished (the last one resets word and done)
+  uint32_t* tmap;            // per ticket: span, its first ticket, T | lg << 24, gen
+  uint32_t* part;            // per ticket: partial register
+  uint32_t* cdone;           // per span, at its first ticket: tickets finished
+  uint32_t* stats;           // cumulative: tickets adopted, spans folded whole, tickets claimed early / late
+  uint32_t cap;              // tickets
+  uint32_t gen;              // this call's generation: tmap entries of earlier calls never match
+  uint32_t dbg;              // test hook: bit 0 delays every push by ~100 us (claims run out first: orphans)
+};
+
 constexpr uint32_t kMaxPlanBlocks = 4096;
+constexpr uint32_t kSlicesPerStream = 16;  // span kernel: task-balanced slices shrink until every stream gets this many
 constexpr uint64_t kMaxGenericSpans = 1ull << 30;  // per generic-path launch sequence
 constexpr uint32_t kPlanThreads = 256;
 
@@ -164,8 +173,9 @@ hipError_t launch_plan(const SpanBatch& a, bool desc, const SplitWs& ws, hipStre
 hipError_t launch_slices(const SpanBatch& a, const SplitWs& ws, hipStream_t s);
 hipError_t launch_combine(const SpanBatch& a, bool desc, bool verify, const SplitWs& ws,
                           hipStream_t s);
-hipError_t launch_quad(const SpanBatch& a, bool verify, int grid, const SplitWs& ws, hipStream_t s);
+hipError_t launch_lane(const SpanBatch& a, bool verify, int grid, const SplitWs& ws, hipStream_t s);
 constexpr int kListThreads = 1024;  // crc32c_long_list_kernel block: one atomic per 16 runs
+hipError_t launch_direct(const SpanBatch& a, bool verify, int grid, const DirectWs& d, hipStream_t s);
 hipError_t launch_scatter(const SpanBatch& a, const SplitWs& ws, const uint32_t* qout, const uint8_t* qmm,
                           hipStream_t s);
 

@@ -1,0 +1,561 @@
+// crc32c_direct.hip -- descriptor batches in ONE launch (n <= kDirectMaxSpans).
+//
+// PrismDB checksums one SST file at a time: TableBuilder::Finish seals ~16.8 K
+// data blocks and an index block (table/table_builder.cc:185-261, called from
+// DoCompactionWork, db/db_impl.cc:2220-2278), and a compaction's input files
+// are verified block by block (ReadBlock, table/format.cc:91-102).  The
+// planner path (crc32c_kernels.hip: memset, plan, slice scan and mark, span
+// pass, segment pass, combine) spends 5-7 launches of 4-6 us each on ~10 us of
+// data at that size.  This kernel does a file in one launch, 8 waves per CU:
+//
+//   static run   wave w owns ~n / nwaves consecutive spans (<= 64; lane j
+//                holds span j's descriptor).  Its spans of one 4 KiB chunk
+//                (all the data blocks of an SST) go through an inline-asm
+//                ring of two slots x two streams -- the streams take
+//                alternate spans, so each fold reads two adjacent blocks, as
+//                the fixed kernel's pairs do -- with counted vmcnt waits and
+//                one coalesced store of the run's results.
+//   long spans   (more than one chunk) are found by their run's wave before
+//                anything else and cut into T tickets of g = 2^lg chunks (the
+//                smallest g <= 8 that gives T <= 64; the first ticket takes
+//                the remainder).  The wave pushes all its tickets with ONE
+//                64-bit atomic on word = supply << 32 | claimed and writes
+//                the ticket map (span, first ticket, T | lg, gen).
+//   tickets      every wave claims up to two tickets right after loading the
+//                tables (so a long span's chunks go out with the first loads
+//                and its combine is off the kernel's tail), and claims again,
+//                one at a time, after its static run until none is left.
+//
+// A claim is one atomicAdd of k on word: tickets [C, C + k) below the supply
+// S are the claimer's.  Tickets >= S were taken before they existed
+// ("orphans"): the wave that pushes them later sees claimed > its first ticket
+// and does those itself.  So no wave ever waits for another wave's progress,
+// except for a ticket-map entry that a running wave is writing (its push came
+// before the claim).  A ticket folds its chunks into a partial register R_k
+// (ticket 0 from the span's initial register, the others from 0) with plain
+// compiler-scheduled buffer loads; the wave that finishes a span's last ticket
+// (per-span counter) combines R = sum_k M^(T-1-k) R_k, M = shift_{4 KiB g},
+// lane-parallel as crc32c_combine_kernel does, feeds the tail bytes and stores
+// the results.  The last group to finish resets word and the group counter
+// for the next call on the stream (the workspace is per (thread, stream)).  If
+// the ticket workspace is full, the discovering wave folds its long spans
+// whole.
+#include "crc32c_fold.h"
+
+namespace prismdb {
+namespace dev {
+
+namespace {
+
+// Chunks per ticket: 2^lg, the smallest power of two <= 8 that keeps a span
+// at <= 64 tickets (one Horner step in the combine).
+__device__ __forceinline__ uint32_t ticket_lg(uint32_t nch) {
+  const uint32_t per = (nch + 63u) >> 6;  // ceil(nch / 64)
+  return per <= 1u ? 0u : (per <= 2u ? 1u : (per <= 4u ? 2u : 3u));
+}
+
+__device__ __forceinline__ uint32_t load_relaxed(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t load_acquire(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Exclusive prefix sum of v over the wave; total = the sum.
+__device__ __forceinline__ uint32_t wave_excl_sum(uint32_t v, uint32_t lane, uint32_t& total) {
+  uint32_t x = v;
+#pragma unroll
+  for (int dd = 1; dd < 64; dd <<= 1) {
+    const uint32_t y = (uint32_t)__shfl_up((int)x, (unsigned)dd, 64);
+    x += lane >= (uint32_t)dd ? y : 0u;
+  }
+  total = readlane(x, 63);
+  return x - v;
+}
+
+enum : uint32_t { kKindNone = 0, kKindStatic = 1 };
+
+// Wave-uniform span geometry, and the chunks [c, c1) a group folds (a ticket
+// of a long span, or all of it).  Chunk k is 4 KiB of body words; chunk 0 is
+// right-aligned (pad leading zero words), so only it is short.
+struct DTask {
+  uint64_t body;  // first 4-B aligned byte of the span
+  uint32_t z;     // body bytes (4 W)
+  uint32_t f;     // pad | h << 10 | t << 12 | kind << 14 | result lane << 17 (static run)
+  uint32_t b;     // span
+  uint32_t c;     // first chunk
+  uint32_t c1;    // one past the last chunk
+  __device__ uint32_t pad() const { return f & 1023u; }
+  __device__ uint32_t h() const { return (f >> 10) & 3u; }
+  __device__ uint32_t t() const { return (f >> 12) & 3u; }
+  __device__ bool valid() const { return ((f >> 14) & 3u) != kKindNone; }
+  __device__ uint32_t slot() const { return f >> 17; }
+  __device__ uint32_t len() const { return h() + z + t(); }
+};
+
+// Span geometry: body, body bytes, pad | h << 10 | t << 12, chunks.
+__device__ __forceinline__ DTask geometry(uint64_t p, uint32_t len) {
+  DTask t;
+  uint32_t h = (4u - ((uint32_t)p & 3u)) & 3u;
+  h = h < len ? h : len;
+  const uint32_t W = (len - h) >> 2, tl = (len - h) & 3u;
+  const uint32_t nch = W ? (W + 1023u) >> 10 : 1u;
+  t.body = p + h;
+  t.z = 4u * W;
+  t.f = (((nch << 10) - W) & 1023u) | (h << 10) | (tl << 12);
+  t.b = 0;
+  t.c = 0;
+  t.c1 = nch;
+  return t;
+}
+
+}  // namespace
+
+// 8 waves per CU (one group: the tables take all of LDS): 256 VGPRs per lane
+// for the ring, the run's descriptors and the combine; 2048 waves keep
+// 8 tasks x 4 KiB in flight each, 64 MiB over the chip, which HBM needs far
+// less of (8 TB/s x ~2 us).
+constexpr uint32_t kDirectWaves = kDirectThreads / 64u;
+
+template <bool kVerify>
+__global__ __launch_bounds__(kDirectThreads) void crc32c_direct_kernel(SpanBatch a, DirectWs d) {
+  const uint32_t n = (uint32_t)a.n;  // <= kDirectMaxSpans, <= 64 per wave
+  const uint32_t tid = threadIdx.x;
+  const uint32_t lane = tid & 63u;
+  const uint32_t wave = rfl(blockIdx.x * kDirectWaves + (tid >> 6));
+  const uint32_t nwaves = gridDim.x * kDirectWaves;
+  const bool hdr = (a.flags & kFlagLogHeader) != 0;
+  const bool has_init = a.init != nullptr;
+  const uint64_t base = reinterpret_cast<uint64_t>(a.base);
+  __shared__ uint32_t lds[kLdsWords];
+
+  // ---- the wave's static run: pairs [plo, phi) -> spans [sbase, sbase + m),
+  // m <= 64; lane j holds span sbase + j's descriptor
+  const uint32_t np = (n + 1u) >> 1;
+  const uint32_t K = np < nwaves ? np : nwaves;
+  uint32_t sbase = 0, m = 0;
+  if (wave < K) {
+    const uint32_t q = np / K, r = np % K;
+    const uint32_t plo = wave * q + (wave < r ? wave : r);
+    const uint32_t phi = plo + q + (wave < r ? 1u : 0u);
+    sbase = 2u * plo;
+    m = (2u * phi < n ? 2u * phi : n) - sbase;
+  }
+  uint32_t voff_lo = 0, voff_hi = 0, vlen = 0, vinit = 0;
+  if (lane < m) {
+    const uint64_t off = a.off[sbase + lane];
+    voff_lo = (uint32_t)off;
+    voff_hi = (uint32_t)(off >> 32);
+    vlen = a.len[sbase + lane];
+    if (has_init) vinit = a.init[sbase + lane];
+  }
+
+  // ---- 1. discovery: the run's long spans (more than one chunk) -> tickets
+  uint32_t adopt_lo = 0, adopt_hi = 0;  // orphans of this wave's push: its own to do
+  uint64_t whole = 0;                   // workspace full: these run spans are folded whole here
+  uint64_t lm = 0;                      // the run's long spans
+  {
+    const uint64_t p = base + (((uint64_t)voff_hi << 32) | voff_lo);
+    const DTask g = geometry(p, vlen);
+    const bool lng = lane < m && g.c1 > 1u;
+    uint32_t T = 0, lg = 0;
+    if (lng) {
+      lg = ticket_lg(g.c1);
+      T = (g.c1 + (1u << lg) - 1u) >> lg;
+    }
+    lm = __ballot(lng);
+    if (lm != 0u) {
+      uint32_t total = 0;
+      const uint32_t ex = wave_excl_sum(T, lane, total);
+      if (d.dbg & 1u) {  // test hook: push late, after other waves have run out of claims
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        while (__builtin_amdgcn_s_memrealtime() - t0 < 10000u) __builtin_amdgcn_s_sleep(64);
+      }
+      uint64_t old = 0;
+      if (lane == 0)
+        old = __hip_atomic_fetch_add(d.word, (unsigned long long)total << 32, __ATOMIC_ACQ_REL,
+                                     __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t S0 = readlane((uint32_t)(old >> 32), 0), C0 = readlane((uint32_t)old, 0);
+      if ((uint64_t)S0 + total <= d.cap) {
+        // the ticket map, one long span at a time, 64 entries per step; the
+        // generation word is stored last (release), claimers spin on it
+        uint64_t mm = lm;
+        while (mm != 0u) {
+          const uint32_t src = (uint32_t)__builtin_ctzll(mm);
+          mm &= mm - 1u;
+          const uint32_t f0 = S0 + readlane(ex, src), Ts = readlane(T, src), lgs = readlane(lg, src);
+          for (uint32_t k = lane; k < Ts; k += 64u) {
+            uint32_t* e = d.tmap + 4ull * (f0 + k);
+            e[0] = sbase + src;
+            e[1] = f0;
+            e[2] = Ts | (lgs << 24);
+            __hip_atomic_store(e + 3, d.gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+          }
+        }
+        if (C0 > S0) {
+          adopt_lo = S0;
+          adopt_hi = C0 < S0 + total ? C0 : S0 + total;
+          if (lane == 0) atomicAdd(d.stats + 0, adopt_hi - adopt_lo);
+        }
+      } else {
+        // no room: claimers skip these tickets (null entries; those past the
+        // workspace are null by position) and this wave folds the spans whole
+        whole = lm;
+        if (lane == 0) atomicAdd(d.stats + 1, (uint32_t)__popcll(lm));
+        const uint32_t hi = (uint64_t)S0 + total < d.cap ? S0 + total : d.cap;
+        for (uint32_t k = S0 + lane; k < hi; k += 64u) {
+          uint32_t* e = d.tmap + 4ull * k;
+          e[0] = kNullSpan;
+          __hip_atomic_store(e + 3, d.gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+    }
+  }
+
+  // A group without static work, adopted tickets, whole spans or visible
+  // tickets leaves before loading the tables.  (The OR over the group goes
+  // through the table area: the tables take all of LDS.)
+  bool work = m != 0u || adopt_lo < adopt_hi;
+  if (!work && lane == 0) {
+    const uint64_t wd = __hip_atomic_load(d.word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    work = (uint32_t)(wd >> 32) > (uint32_t)wd;
+  }
+  const bool wwork = __ballot(work) != 0u;
+  if (lane == 0) lds[tid >> 6] = wwork ? 1u : 0u;
+  __syncthreads();
+  uint32_t any = 0;
+#pragma unroll
+  for (int k = 0; k < (int)kDirectWaves; ++k) any |= lds[k];
+  __syncthreads();
+  if (any != 0u) {
+    load_tables<kDirectThreads>(lds, a.tabs, tid);
+    __syncthreads();
+    const StrideLanes tab = stride_lanes(lane);
+    const uint32_t nibtab = 4u * (kTabWords + lane);
+    const ShortShift ss = short_shift_cols(lane);
+    uint32_t res = 0u, bad = 0u, have = 0u;  // the static run's results: lane j = span sbase + j
+
+    // The span's crc from its body register (or, without body words, from
+    // its initial register): tail bytes, conditioning, Mask; the result, the
+    // verify flag and the trailer.  A span of the static run keeps its result
+    // in lane `slot` for the run's one coalesced store; the others' results
+    // are stored by lane 0.
+    auto finish = [&](const DTask& t, uint32_t reg, uint32_t tail, uint32_t stored, bool to_run) {
+      const uint32_t tl = t.t();
+      const uint32_t crc = feed_short(ss, lane, reg, tail, tl) ^ kConditioning;
+      const uint32_t v = (a.flags & kFlagMask) ? mask_crc(crc) : crc;
+      const uint32_t mm = crc != unmask_crc(stored) ? 1u : 0u;
+      if (to_run) {
+        const uint32_t slot = t.slot();
+        res = lane == slot ? v : res;
+        if (kVerify) bad = lane == slot ? mm : bad;
+        have = lane == slot ? 1u : have;
+      } else if (lane == 0) {
+        if (a.out != nullptr) a.out[t.b] = v;
+        if (kVerify && a.mismatch != nullptr) a.mismatch[t.b] = (uint8_t)mm;
+      }
+      if ((a.flags & kFlagWriteTrailer) && lane == 0) {
+        const uint64_t start = t.body - t.h();
+        store_le32(reinterpret_cast<const uint8_t*>(hdr ? start - kLogCrcBack : t.body + t.z + tl), v);
+      }
+    };
+    // the edge bytes read by lanes 0-9 (head, tail, stored crc) as words
+    auto edge_head = [&](uint32_t e, uint32_t h) -> uint32_t {
+      return h ? readlane(e, 0) | (readlane(e, 1) << 8) | (readlane(e, 2) << 16) : 0u;
+    };
+    auto edge_tail = [&](uint32_t e, uint32_t tl) -> uint32_t {
+      return tl ? readlane(e, 3) | (readlane(e, 4) << 8) | (readlane(e, 5) << 16) : 0u;
+    };
+    auto edge_stored = [&](uint32_t e) -> uint32_t {
+      return kVerify ? readlane(e, 6) | (readlane(e, 7) << 8) | (readlane(e, 8) << 16) | (readlane(e, 9) << 24) : 0u;
+    };
+    // The register enters with body word 0: lane pad % 64 of round pad / 64
+    // (a wave-uniform round: a masked XOR per round, no indexed access).
+    auto inject = [&](uint32_t (&w)[kRounds], uint32_t pad, uint32_t rr) {
+      const uint32_t J = pad >> 6;
+      const uint32_t inj = lane == (pad & 63u) ? rr : 0u;
+      if (J == 0) {
+        w[0] ^= inj;
+      } else {
+#pragma unroll
+        for (int j = 1; j < kRounds; ++j) w[j] = __builtin_amdgcn_bitop3_b32(w[j], inj, (uint32_t)j == J ? ~0u : 0u, 0x78);
+      }
+    };
+
+    // ---- groups: tickets and whole spans.  Compiler-scheduled buffer loads
+    // (outside the body they read 0: chunk 0's right-aligned padding), two
+    // chunks per step.  Rare next to the static run (an SST file has one long
+    // span), so this loop favours simplicity over the ring's overlap.
+    // Returns the register over chunks [t.c, t.c1) -- from the span's initial
+    // register when t.c == 0, else from 0 -- and in r0 the initial register.
+    auto group_reg = [&](const DTask& t, uint32_t init, uint32_t& r0) -> uint32_t {
+      const __amdgpu_buffer_rsrc_t rb =
+          __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(t.body), (short)0, (int)t.z, 0x00020000);
+      const uint32_t pad = t.pad(), h = t.h();
+      r0 = 0u;
+      if (t.c == 0u) {
+        const uint8_t* sp = reinterpret_cast<const uint8_t*>(t.body - h);
+        const uint32_t hb = lane < h ? (uint32_t)sp[lane] : 0u;
+        r0 = feed_short(ss, lane, init ^ kConditioning, edge_head(hb, h), h);
+      }
+      uint32_t acc = 0u;
+      for (uint32_t c = t.c; c < t.c1; c += 2u) {
+        const bool two = c + 1u < t.c1;
+        uint32_t w0[kRounds], w1[kRounds];
+        const uint32_t i0 = (c << 10) + lane - pad;  // may wrap: out of range, reads 0
+#pragma unroll
+        for (int j = 0; j < kRounds; ++j) {
+          w0[j] = __builtin_amdgcn_raw_buffer_load_b32(rb, (int)((i0 + 64u * (uint32_t)j) * 4u), 0, 0);
+          w1[j] = two ? __builtin_amdgcn_raw_buffer_load_b32(rb, (int)((i0 + 1024u + 64u * (uint32_t)j) * 4u), 0, 0)
+                      : 0u;
+        }
+        if (c == 0u && t.z != 0u) inject(w0, pad, r0);
+#pragma unroll
+        for (int j = 0; j < kRounds; ++j) acc = step256(lds, tab, acc, w0[j]);
+        if (two) {
+#pragma unroll
+          for (int j = 0; j < kRounds; ++j) acc = step256(lds, tab, acc, w1[j]);
+        }
+      }
+      return wave_xor(realign(lds, nibtab, acc));
+    };
+    // tail bytes and the stored crc of a span, read directly
+    auto span_edges = [&](const DTask& t, uint32_t& tail, uint32_t& stored) {
+      const uint32_t tl = t.t();
+      const uint64_t start = t.body - t.h();
+      const uint8_t* ep = nullptr;
+      if (lane >= 3u && lane < 3u + tl) ep = reinterpret_cast<const uint8_t*>(t.body + t.z + (lane - 3u));
+      if (kVerify && lane >= 6u && lane < 10u)
+        ep = reinterpret_cast<const uint8_t*>((hdr ? start - kLogCrcBack : t.body + t.z + tl) + (lane - 6u));
+      const uint32_t e = ep != nullptr ? (uint32_t)*ep : 0u;
+      tail = edge_tail(e, tl);
+      stored = edge_stored(e);
+    };
+    // Ticket tkt (< cap): spin until its map entry is this call's, fold its
+    // chunks, store and count the partial; the span's last ticket combines
+    // R = sum_k M^(T-1-k) R_k (M = shift_{4 KiB 2^lg}) and finishes the span.
+    auto run_ticket = [&](uint32_t tkt) {
+      const uint32_t* e = d.tmap + 4ull * tkt;
+      while (rfl(load_acquire(e + 3)) != d.gen) __builtin_amdgcn_s_sleep(2);
+      const uint32_t sb = rfl(load_relaxed(e));
+      if (sb == kNullSpan) return;
+      const uint32_t f0 = rfl(load_relaxed(e + 1)), tn = rfl(load_relaxed(e + 2));
+      DTask t = geometry(base + const_load(a.off, sb), const_load(a.len, sb));
+      t.b = sb;
+      const uint32_t T = tn & 0xFFFFFFu, lg = tn >> 24, k = tkt - f0;
+      const uint32_t first = t.c1 - ((T - 1u) << lg);  // ticket 0: the remainder
+      t.c = k ? first + ((k - 1u) << lg) : 0u;
+      t.c1 = k ? t.c + (1u << lg) : first;
+      uint32_t r0 = 0;
+      const uint32_t v = group_reg(t, (k == 0u && has_init) ? const_load(a.init, sb) : 0u, r0);
+      uint32_t old = 0;
+      if (lane == 0) {
+        __hip_atomic_store(d.part + tkt, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        old = __hip_atomic_fetch_add(d.cdone + f0, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      if (readlane(old, 0) + 1u != T) return;
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      const uint32_t J = (T + 63u) >> 6;
+      const int32_t pad0 = (int32_t)(J * 64u - T);
+      uint32_t x = 0;
+      for (uint32_t j = 0; j < J; ++j) {
+        const int32_t kk = (int32_t)(j * 64u + lane) - pad0;
+        const uint32_t s = kk >= 0 ? load_relaxed(d.part + f0 + (uint32_t)kk) : 0u;
+        x = gf2_apply(a.tabs->tick64[lg], x) ^ s;
+      }
+      uint32_t y = 0;
+#pragma unroll
+      for (int i = 0; i < 32; ++i) y ^= a.tabs->tick_lane[lg][i][lane] & (0u - ((x >> i) & 1u));
+      const uint32_t R = wave_xor(y);
+      if (lane == 0) __hip_atomic_store(d.cdone + f0, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      uint32_t tail = 0, stored = 0;
+      span_edges(t, tail, stored);
+      finish(t, R, tail, stored, false);
+    };
+    // a long span of the run folded whole by this wave (ticket workspace full)
+    auto run_whole = [&](uint32_t j) {
+      const uint64_t off = ((uint64_t)readlane(voff_hi, j) << 32) | readlane(voff_lo, j);
+      DTask t = geometry(base + off, readlane(vlen, j));
+      t.b = sbase + j;
+      uint32_t r0 = 0;
+      const uint32_t R = group_reg(t, readlane(vinit, j), r0);
+      uint32_t tail = 0, stored = 0;
+      span_edges(t, tail, stored);
+      finish(t, t.z ? R : r0, tail, stored, false);
+    };
+    auto claim = [&](uint32_t k, uint32_t& c, uint32_t& sp) {
+      uint64_t old = 0;
+      if (lane == 0)
+        old = __hip_atomic_fetch_add(d.word, (unsigned long long)k, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+      sp = readlane((uint32_t)(old >> 32), 0);
+      c = readlane((uint32_t)old, 0);
+    };
+
+    // ---- early: this wave's orphans, its whole spans, up to two claims
+    for (uint32_t tkt = adopt_lo; tkt < adopt_hi; ++tkt) run_ticket(tkt);
+    for (uint64_t wm = whole; wm != 0u; wm &= wm - 1u) run_whole((uint32_t)__builtin_ctzll(wm));
+    {
+      uint64_t wd = 0;
+      if (lane == 0) wd = __hip_atomic_load(d.word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t S = readlane((uint32_t)(wd >> 32), 0), C = readlane((uint32_t)wd, 0);
+      if (S > C) {
+        const uint32_t k = S - C >= 2u ? 2u : 1u;
+        uint32_t c = 0, sp = 0;
+        claim(k, c, sp);
+        const uint32_t got = sp > c ? (sp - c >= k ? k : sp - c) : 0u;
+        if (lane == 0 && got) atomicAdd(d.stats + 2, got);
+        for (uint32_t i = 0; i < got; ++i)
+          if (c + i < d.cap) run_ticket(c + i);
+      }
+    }
+
+    // ---- the static run: one-chunk spans, stream st taking run positions
+    // st, st + 2, ... (long ones skipped).  Ring of two slots x two streams,
+    // inline-asm loads, counted waits -- crc32c_span_kernel's pair runs.
+    if (m != 0u) {
+      const uint64_t inrun = m >= 64u ? ~0ull : (1ull << m) - 1ull;
+      const uint64_t shortm = inrun & ~lm;
+      // next short span of stream st at or after position j: (slot, geometry)
+      auto static_task = [&](uint32_t& j, uint32_t st) -> DTask {
+        const uint64_t par = st ? 0xAAAAAAAAAAAAAAAAull : 0x5555555555555555ull;
+        const uint64_t from = j >= 64u ? 0ull : ~0ull << j;
+        const uint64_t avail = shortm & par & from;
+        if (avail == 0u) {
+          j = 64u;
+          DTask t = geometry(base, 0u);
+          t.f = 0;  // kind none
+          return t;
+        }
+        const uint32_t p = (uint32_t)__builtin_ctzll(avail);
+        const uint64_t off = ((uint64_t)readlane(voff_hi, p) << 32) | readlane(voff_lo, p);
+        DTask t = geometry(base + off, readlane(vlen, p));
+        t.b = sbase + p;
+        t.f |= (kKindStatic << 14) | (p << 17);
+        j = p + 2u;
+        return t;
+      };
+      // 17 loads per task, always: 16 body dwords (the buffer range check
+      // reads 0 outside the body: chunk 0's padding) and one edge byte per
+      // lane -- head bytes (lanes 0-2), tail bytes (3-5), stored crc (6-9).
+      auto issue = [&](const DTask& t, uint32_t (&w)[kRounds], uint32_t& e) {
+        const bool live = t.valid();
+        const uint32_t pad = t.pad(), h = t.h(), tl = t.t(), len = t.len();
+        const bool hwin = kVerify && hdr;
+        auto sat = [](uint64_t x) -> uint32_t { return x > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)x; };
+        const uint64_t start = t.body - h;
+        u32x4 rb = buffer_rsrc(reinterpret_cast<const uint8_t*>(t.body), live ? t.z : 0u);
+        u32x4 re = buffer_rsrc(reinterpret_cast<const uint8_t*>(hwin ? start - kLogCrcBack : start),
+                               live ? (hwin ? sat((uint64_t)kLogCrcBack + len) : sat((uint64_t)len + (kVerify ? 4u : 0u)))
+                                    : 0u);
+        // SGPRs the vector unit wrote (readlane) need 5 wait states before a
+        // VMEM instruction reads them; hipcc inserts none before inline asm.
+        asm volatile("s_nop 4" : "+s"(rb), "+s"(re));
+        const int32_t i0 = (int32_t)lane - (int32_t)pad;
+        if (pad == 0) {
+          load_rounds(w, rb, (uint32_t)i0 * 4u);
+        } else if (pad <= 64u) {
+          w[0] = buf_dword<0>(rb, (uint32_t)i0 * 4u);
+          load_rounds_from1(w, rb, (uint32_t)(i0 + 64) * 4u);
+        } else {
+#pragma unroll
+          for (int j = 0; j < kRounds; ++j) w[j] = buf_dword<0>(rb, (uint32_t)(i0 + 64 * j) * 4u);
+        }
+        const uint32_t hb = hwin ? kLogCrcBack : 0u;  // edge-window offset of the span's first byte
+        uint32_t eoff = 0xFFFFFFFFu;
+        if (lane < h) eoff = hb + lane;
+        if (lane >= 3u && lane < 3u + tl) eoff = sat((uint64_t)hb + h + t.z + (lane - 3u));
+        if (kVerify && lane >= 6u && lane < 10u) eoff = hwin ? lane - 6u : sat((uint64_t)len + (lane - 6u));
+        e = buf_ubyte(re, eoff);
+      };
+      auto fold = [&](const DTask& tx, uint32_t (&wx)[kRounds], uint32_t ex, const DTask& ty,
+                      uint32_t (&wy)[kRounds], uint32_t ey) {
+        // initial registers (init fed the head bytes) into body word 0
+        const uint32_t rx = feed_short(ss, lane, readlane(vinit, tx.slot()) ^ kConditioning, edge_head(ex, tx.h()), tx.h());
+        const uint32_t ry = feed_short(ss, lane, readlane(vinit, ty.slot()) ^ kConditioning, edge_head(ey, ty.h()), ty.h());
+        if (tx.z) inject(wx, tx.pad(), rx);
+        if (ty.z) inject(wy, ty.pad(), ry);
+        uint32_t ax = 0, ay = 0;
+#pragma unroll
+        for (int j = 0; j < kRounds; ++j) {
+          ax = step256(lds, tab, ax, wx[j]);
+          ay = step256(lds, tab, ay, wy[j]);
+        }
+        const uint32_t vx = realign(lds, nibtab, ax), vy = realign(lds, nibtab, ay);
+        const uint32_t bx = wave_xor(vx), by = wave_xor(vy);
+        if (tx.valid()) finish(tx, tx.z ? bx : rx, edge_tail(ex, tx.t()), edge_stored(ex), true);
+        if (ty.valid()) finish(ty, ty.z ? by : ry, edge_tail(ey, ty.t()), edge_stored(ey), true);
+      };
+      DTask tk[2][2];
+      uint32_t wb[2][2][kRounds];
+      uint32_t eb[2][2];
+      uint32_t j0 = 0, j1 = 1;
+#pragma unroll
+      for (int sl = 0; sl < 2; ++sl) {
+        tk[sl][0] = static_task(j0, 0u);
+        tk[sl][1] = static_task(j1, 1u);
+      }
+      if (tk[0][0].valid() || tk[0][1].valid()) {
+#pragma unroll
+        for (int sl = 0; sl < 2; ++sl) {
+          issue(tk[sl][0], wb[sl][0], eb[sl][0]);
+          issue(tk[sl][1], wb[sl][1], eb[sl][1]);
+        }
+        constexpr int kYounger = 2 * (kRounds + 1);  // the other slot's two tasks
+        for (;;) {
+#pragma unroll
+          for (int sl = 0; sl < 2; ++sl) {
+            wait_task<kYounger>(wb[sl][0], eb[sl][0]);
+            wait_task<kYounger>(wb[sl][1], eb[sl][1]);
+            fold(tk[sl][0], wb[sl][0], eb[sl][0], tk[sl][1], wb[sl][1], eb[sl][1]);
+            if (!tk[sl ^ 1][0].valid() && !tk[sl ^ 1][1].valid()) goto drained;
+            tk[sl][0] = static_task(j0, 0u);
+            tk[sl][1] = static_task(j1, 1u);
+            issue(tk[sl][0], wb[sl][0], eb[sl][0]);
+            issue(tk[sl][1], wb[sl][1], eb[sl][1]);
+          }
+        }
+      drained:
+#pragma unroll
+        for (int sl = 0; sl < 2; ++sl) {
+          wait_task<0>(wb[sl][0], eb[sl][0]);
+          wait_task<0>(wb[sl][1], eb[sl][1]);
+        }
+      }
+    }
+
+    // ---- late: claims, one ticket at a time, until none is left (a claim
+    // past the supply is an orphan: its pusher does it)
+    for (;;) {
+      uint32_t c = 0, sp = 0;
+      claim(1u, c, sp);
+      if (c >= sp) break;
+      if (lane == 0) atomicAdd(d.stats + 3, 1u);
+      if (c < d.cap) run_ticket(c);
+    }
+    // the static run's results: one coalesced store (long spans' lanes are
+    // their completers')
+    if (lane < m && have != 0u) {
+      if (a.out != nullptr) __builtin_nontemporal_store(res, a.out + sbase + lane);
+      if (kVerify && a.mismatch != nullptr) __builtin_nontemporal_store((uint8_t)bad, a.mismatch + sbase + lane);
+    }
+  }
+
+  // The last group to finish resets the counters for the next call.
+  __syncthreads();
+  if (tid == 0) {
+    const uint32_t old = __hip_atomic_fetch_add(d.done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (old + 1u == gridDim.x) {
+      __hip_atomic_store(d.word, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(d.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+hipError_t launch_direct(const SpanBatch& a, bool verify, int grid, const DirectWs& d, hipStream_t s) {
+  if (verify) crc32c_direct_kernel<true><<<grid, kDirectThreads, 0, s>>>(a, d);
+  else crc32c_direct_kernel<false><<<grid, kDirectThreads, 0, s>>>(a, d);
+  return hipGetLastError();
+}
+
+}  // namespace dev
+}  // namespace prismdb

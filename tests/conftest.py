@@ -130,3 +130,42 @@ def native():
 
         build()
     return _lib.lib()
+
+
+# Descriptor-batch routes the GPU tests pin (C-ABI test hooks, not public):
+#   direct     the one-launch kernel (crc32c_direct.hip; the default for
+#              batches of <= 2^17 spans)
+#   lane_log   the planner path, lane kernel in front of log-record batches
+#              (the default for larger batches)
+#   lane_all   the planner path, lane kernel in front of every batch
+#   span_only  the planner path alone
+ROUTES = {"direct": (1 << 17, 0), "lane_log": (0, 0), "lane_all": (0, 1), "span_only": (0, -1)}
+
+
+def set_route(native, name):
+    """Pin a route; returns a callable restoring the defaults."""
+    direct_max, lane = ROUTES[name]
+    native.prismdb_crc32c_direct_max(direct_max)
+    native.prismdb_crc32c_lane_mode(lane)
+
+    def restore():
+        native.prismdb_crc32c_direct_max(1 << 17)
+        native.prismdb_crc32c_lane_mode(0)
+
+    return restore
+
+
+@pytest.fixture(params=["direct", "lane_log"])
+def route(request, native):
+    """The two default descriptor routes: one-launch and planner."""
+    restore = set_route(native, request.param)
+    yield request.param
+    restore()
+
+
+@pytest.fixture(params=list(ROUTES))
+def any_route(request, native):
+    """Every descriptor route."""
+    restore = set_route(native, request.param)
+    yield request.param
+    restore()

@@ -1,0 +1,276 @@
+"""The one-launch descriptor path (prismdb_amd/csrc/crc32c_direct.hip) at the
+granularity PrismDB calls at: one SST file per call (TableBuilder::Finish,
+table/table_builder.cc:185-261; ReadBlock verify over a compaction input,
+table/format.cc:91-102), many calls back to back on one stream; and its
+machinery: tickets of long spans claimed by any wave, the combine, the
+whole-span fallback when the ticket workspace is full, orphaned claims
+adopted by a late pusher.  Bit-exact against the oracle."""
+import ctypes
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ND, DATA, STRIDE, INDEX = 16811, 3988, 3992, 486977  # one 64 MiB-class SST
+
+
+@pytest.fixture(scope="module")
+def dev(native):
+    import torch
+
+    assert torch.cuda.is_available(), "gpu tests need a HIP device"
+    from prismdb_amd import crc32c
+
+    crc32c.device_init(0)
+    return torch.device("cuda", 0)
+
+
+def _u32(t):
+    return t.cpu().numpy().view(np.uint32)
+
+
+def _stats(native):
+    arr = (ctypes.c_uint64 * 4)()
+    assert native.prismdb_crc32c_direct_stats(arr) == 0
+    return np.array(arr, dtype=np.int64)
+
+
+def _last_split_rc(native):
+    arr = (ctypes.c_uint64 * 4)()
+    return native.prismdb_crc32c_last_split(arr)
+
+
+def _sst_file(oracle, seed, files=1):
+    """`files` SST-shaped files back to back: per file 16 811 data spans
+    (contents || type, 3988 B at stride 3992) and the index span, each with
+    its masked crc stored after it (a sealed file).  Returns host bytes,
+    offsets, lengths and the masked crcs."""
+    fbytes = ND * STRIDE + INDEX + 4
+    off1 = np.concatenate([np.arange(ND, dtype=np.uint64) * STRIDE, [ND * STRIDE]])
+    len1 = np.concatenate([np.full(ND, DATA, dtype=np.uint32), [INDEX]])
+    host = oracle.synth(files * fbytes + 64, seed)
+    off = (np.arange(files, dtype=np.uint64)[:, None] * fbytes + off1[None, :]).reshape(-1) + 8
+    lens = np.tile(len1, files)
+    raw, _ = oracle.batch(host, off, lens)
+    masked = np.array([oracle.mask(int(c)) for c in raw], dtype=np.uint32)
+    tr = (off + lens.astype(np.uint64)).astype(np.int64)[:, None] + np.arange(4)[None, :]
+    host[tr] = masked.astype("<u4").view(np.uint8).reshape(-1, 4)
+    return host, off, lens, raw, masked
+
+
+def test_sst_file_calls_back_to_back(dev, oracle, native):
+    """100 single-file calls enqueued back to back on one stream, alternating
+    WriteRawBlock sealing (MASK | WRITE_TRAILER: rewrites the same trailers)
+    and ReadBlock verify, each into its own result arrays; every result of
+    every call against the oracle.  The calls take the one-launch path."""
+    import torch
+    from prismdb_amd import crc32c
+
+    host, off, lens, raw, masked = _sst_file(oracle, 0x5EED00D1)
+    buf = torch.from_numpy(host).to(dev)
+    d_off = torch.from_numpy(off.astype(np.int64)).to(dev)
+    d_len = torch.from_numpy(lens.view(np.int32)).to(dev)
+    n = len(off)
+    calls = 100
+    outs = torch.empty((calls, n), dtype=torch.int32, device=dev)
+    mms = torch.full((calls, n), 7, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+    for i in range(calls):
+        if i % 2 == 0:
+            crc32c.batch(buf, d_off, d_len, mask=True, trailer=True, out=outs[i], check_bounds=False)
+        else:
+            crc32c.batch(buf, d_off, d_len, verify=True, out=outs[i], mismatch=mms[i], check_bounds=False)
+    torch.cuda.synchronize()
+    assert _last_split_rc(native) == -2  # the one-launch path
+    got = outs.cpu().numpy().view(np.uint32)
+    for i in range(calls):
+        np.testing.assert_array_equal(got[i], masked if i % 2 == 0 else raw, err_msg=f"call {i}")
+    mm = mms.cpu().numpy()
+    assert (mm[1::2] == 0).all()
+    assert (buf.cpu().numpy() == host).all()  # the trailers written equal the stored ones
+
+
+@pytest.mark.parametrize("files", [1, 7])
+def test_sst_files_verify_damaged(dev, oracle, native, files):
+    """Verify one and seven files per call (7 x 16 812 spans: the one-launch
+    limit is 2^17) with damaged data blocks, a damaged index block (its
+    tickets) and a damaged trailer; a non-zero init on every span."""
+    import torch
+    from prismdb_amd import crc32c
+
+    host, off, lens, raw, masked = _sst_file(oracle, 0x5EED00D2 + files, files)
+    n = len(off)
+    victims = [3, n - 1, (n // 2) | 1, ND]  # data blocks, the last file's index, the first file's index
+    for v in victims[:3]:
+        host[int(off[v]) + int(lens[v]) // 3] ^= 0x11
+    host[int(off[victims[3]]) + int(lens[victims[3]]) + 1] ^= 0x80  # trailer byte
+    init = (np.arange(n, dtype=np.uint64) * 0x9E3779B1 % (1 << 32)).astype(np.uint32)
+    want, wmm = oracle.batch(host, off, lens, init, mask=True, verify=True)
+    buf = torch.from_numpy(host).to(dev)
+    out, mm = crc32c.batch(buf, torch.from_numpy(off.astype(np.int64)).to(dev),
+                           torch.from_numpy(lens.view(np.int32)).to(dev),
+                           torch.from_numpy(init.view(np.int32)).to(dev), mask=True, verify=True)
+    assert _last_split_rc(native) == -2
+    np.testing.assert_array_equal(_u32(out), want)
+    np.testing.assert_array_equal(mm.cpu().numpy(), wmm)
+    assert sorted(np.flatnonzero(mm.cpu().numpy()).tolist()) == sorted(set(victims))
+
+
+def test_tickets_claimed_and_combined(dev, oracle, native):
+    """Long spans of every ticket size (1, 2, 4 and 8 chunks per ticket, up to
+    128 tickets: a two-step combine) mixed with short ones, at odd offsets,
+    random init, MASK; the counters account for every ticket (claimed early,
+    late or adopted) and no span was folded whole."""
+    import torch
+    from prismdb_amd import crc32c
+
+    rng = np.random.default_rng(0x5EED00D3)
+    long_lens = [4097, 8192 + 5, 64 * 4096 + 1, 65 * 4096, 300_001, 1 << 20, (4 << 20) + 3, 2 * 4096 * 64 + 7]
+    lens = np.concatenate([rng.integers(0, 4097, size=3000), long_lens]).astype(np.uint64)
+    rng.shuffle(lens)
+    gaps = rng.integers(0, 9, size=len(lens)).astype(np.uint64)
+    off = np.cumsum(np.concatenate([[5], (lens + gaps)[:-1]])).astype(np.uint64)
+    host = oracle.synth(int(off[-1] + lens[-1]) + 16, 0x5EED00D4)
+    init = rng.integers(0, 2**32, size=len(lens), dtype=np.uint64).astype(np.uint32)
+    want, _ = oracle.batch(host, off, lens, init, mask=True)
+
+    def tickets(L, o):
+        h = (4 - (8 + o) % 4) % 4  # the device buffer starts 256-B aligned
+        h = min(h, L)
+        W = (L - h) // 4
+        nch = (W + 1023) // 1024
+        if nch <= 1:
+            return 0
+        per = (nch + 63) // 64
+        lg = 0 if per <= 1 else 1 if per <= 2 else 2 if per <= 4 else 3
+        return (nch + (1 << lg) - 1) >> lg
+
+    buf = torch.empty(len(host) + 8, dtype=torch.uint8, device=dev)
+    buf[8:] = torch.from_numpy(host).to(dev)
+    d_off = torch.from_numpy((off + 8).astype(np.int64)).to(dev)
+    d_len = torch.from_numpy(lens.astype(np.uint32).view(np.int32)).to(dev)
+    d_init = torch.from_numpy(init.view(np.int32)).to(dev)
+    crc32c.batch(buf, d_off[:1], d_len[:1])  # this thread's workspace exists
+    before = _stats(native)
+    out, _ = crc32c.batch(buf, d_off, d_len, d_init, mask=True)
+    after = _stats(native)
+    np.testing.assert_array_equal(_u32(out), want)
+    expect = sum(tickets(int(L), int(o)) for L, o in zip(lens, off))
+    d = after - before
+    assert d[1] == 0  # no span folded whole
+    assert d[0] + d[2] + d[3] == expect, (d, expect)
+
+
+def test_ticket_workspace_full_whole_spans(dev, oracle, native):
+    """A ticket workspace of 16 entries: the first pushes fit, the rest spill
+    to whole-span folding by their discovering wave; claims of null tickets
+    are skipped.  Results still bit-exact."""
+    import torch
+    from prismdb_amd import crc32c
+
+    rng = np.random.default_rng(0x5EED00D5)
+    lens = rng.integers(4100, 400_000, size=300).astype(np.uint64)
+    lens[::3] = rng.integers(0, 4000, size=len(lens[::3]))
+    off = np.cumsum(np.concatenate([[3], (lens + 5)[:-1]])).astype(np.uint64)
+    host = oracle.synth(int(off[-1] + lens[-1]) + 16, 0x5EED00D6)
+    want, _ = oracle.batch(host, off, lens)
+    buf = torch.from_numpy(host).to(dev)
+    d_off = torch.from_numpy(off.astype(np.int64)).to(dev)
+    d_len = torch.from_numpy(lens.astype(np.uint32).view(np.int32)).to(dev)
+    crc32c.batch(buf, d_off[:1], d_len[:1])
+    before = _stats(native)
+    prev = native.prismdb_crc32c_direct_tickets(16)
+    try:
+        out, _ = crc32c.batch(buf, d_off, d_len)
+        got = _u32(out)
+        after = _stats(native)
+    finally:
+        native.prismdb_crc32c_direct_tickets(prev)
+    np.testing.assert_array_equal(got, want)
+    assert (after - before)[1] > 0  # spans folded whole
+    out2, _ = crc32c.batch(buf, d_off, d_len)  # full workspace again
+    np.testing.assert_array_equal(_u32(out2), want)
+
+
+def test_orphaned_claims_adopted(dev, oracle, native):
+    """Pushes delayed ~100 us (test hook): the other waves finish their runs
+    and claim past the supply first; the late pusher finds its tickets claimed
+    by waves that left (orphans) and folds them itself.  An SST file with
+    sealed trailers, verify."""
+    import torch
+    from prismdb_amd import crc32c
+
+    host, off, lens, raw, masked = _sst_file(oracle, 0x5EED00D7)
+    buf = torch.from_numpy(host).to(dev)
+    d_off = torch.from_numpy(off.astype(np.int64)).to(dev)
+    d_len = torch.from_numpy(lens.view(np.int32)).to(dev)
+    crc32c.batch(buf, d_off[:1], d_len[:1])
+    before = _stats(native)
+    prev = native.prismdb_crc32c_direct_debug(1)
+    try:
+        out, mm = crc32c.batch(buf, d_off, d_len, verify=True, check_bounds=False)
+        got, gmm = _u32(out), mm.cpu().numpy()
+        after = _stats(native)
+    finally:
+        native.prismdb_crc32c_direct_debug(prev)
+    np.testing.assert_array_equal(got, raw)
+    assert (gmm == 0).all()
+    assert (after - before)[0] > 0  # tickets adopted
+
+
+def test_direct_limit(dev, oracle, native):
+    """2^17 spans (the one-launch limit) take the one-launch path, 2^17 + 1 the
+    planner; both bit-exact on the same mix of short and long spans."""
+    import torch
+    from prismdb_amd import crc32c
+
+    rng = np.random.default_rng(0x5EED00D8)
+    size = 64 << 20
+    host = oracle.synth(size, 0x5EED00D8)
+    for n, rc in ((1 << 17, -2), ((1 << 17) + 1, 0)):
+        lens = rng.integers(0, 4500, size=n).astype(np.uint64)
+        lens[rng.integers(0, n, size=20)] = rng.integers(4500, 200_000, size=20)
+        off = rng.integers(0, size - 200_001, size=n).astype(np.uint64)
+        want, _ = oracle.batch(host, off, lens)
+        out, _ = crc32c.batch(torch.from_numpy(host).to(dev), torch.from_numpy(off.astype(np.int64)).to(dev),
+                              torch.from_numpy(lens.astype(np.uint32).view(np.int32)).to(dev))
+        assert _last_split_rc(native) == rc
+        np.testing.assert_array_equal(_u32(out), want)
+
+
+def test_direct_concurrent_threads(dev, oracle):
+    """Four host threads on their own streams, each enqueuing 20 one-launch
+    file-sized batches back to back (per-(thread, stream) ticket workspaces and
+    counters), then checking all of them."""
+    import threading
+
+    import torch
+    from prismdb_amd import crc32c
+
+    host, off, lens, raw, masked = _sst_file(oracle, 0x5EED00D9)
+    buf = torch.from_numpy(host).to(dev)
+    d_off = torch.from_numpy(off.astype(np.int64)).to(dev)
+    d_len = torch.from_numpy(lens.view(np.int32)).to(dev)
+    errors = []
+
+    def run(t):
+        try:
+            s = torch.cuda.Stream()
+            with torch.cuda.stream(s):
+                outs = torch.empty((20, len(off)), dtype=torch.int32, device=dev)
+                for i in range(20):
+                    crc32c.batch(buf, d_off, d_len, mask=bool(t & 1), out=outs[i], check_bounds=False, stream=s)
+                s.synchronize()
+                want = masked if t & 1 else raw
+                if not (outs.cpu().numpy().view(np.uint32) == want[None, :]).all():
+                    errors.append(t)
+        except Exception as e:  # noqa: BLE001 - reported below
+            errors.append((t, repr(e)))
+
+    th = [threading.Thread(target=run, args=(t,)) for t in range(4)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join(120)
+    assert not errors, errors

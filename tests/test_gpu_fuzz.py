@@ -1,9 +1,9 @@
 """Randomized parity of the batch engine against the oracle: random span
 geometries (empty to split-path lengths, any alignment, overlapping), random
 flags (MASK, verify, WRITE_TRAILER, LOG_HEADER) and random fixed-stride
-shapes, on the fast and on the generic kernel, and descriptor batches with
-the short-record (quad) kernel in front of the generic path for every batch,
-for log batches only (the default) and for none.  Bit-exact.
+shapes, on the fast and on the generic kernel, and descriptor batches on
+every route: the one-launch kernel, and the planner path with the lane kernel
+in front of every batch, of log batches only, or of none.  Bit-exact.
 
 Expected values come from the oracle (oracle/crc32c_oracle.c, pinned to the
 reference's golden vectors) on the same bytes; what a flag adds is checked
@@ -34,17 +34,6 @@ def dev(native):
     return torch.device("cuda", 0)
 
 
-@pytest.fixture(params=[0, 1, -1], ids=["quad_log", "quad_all", "quad_off"])
-def quad_mode(request, native):
-    """prismdb_crc32c_quad_mode: which descriptor batches take the quad kernel."""
-    import ctypes
-
-    native.prismdb_crc32c_quad_mode.argtypes = [ctypes.c_int]
-    native.prismdb_crc32c_quad_mode(request.param)
-    yield request.param
-    native.prismdb_crc32c_quad_mode(0)
-
-
 def _u32(t):
     return t.cpu().numpy().view(np.uint32)
 
@@ -64,7 +53,7 @@ def _lengths(rng, n):
 
 
 @pytest.mark.parametrize("seed", SEEDS)
-def test_random_spans(dev, oracle, quad_mode, seed):
+def test_random_spans(dev, oracle, any_route, seed):
     import torch
     from prismdb_amd import crc32c
 
@@ -100,7 +89,7 @@ def test_random_spans(dev, oracle, quad_mode, seed):
 
 
 @pytest.mark.parametrize("seed", SEEDS[:12])
-def test_random_trailer_sealing(dev, oracle, quad_mode, seed):
+def test_random_trailer_sealing(dev, oracle, any_route, seed):
     """WRITE_TRAILER on disjoint spans (a trailer must not land in another
     span): every trailer is LE32(Mask(crc)) or the raw crc, per MASK; bytes
     outside the trailers are untouched; LOG_HEADER writes 6 bytes before."""

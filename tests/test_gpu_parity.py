@@ -25,13 +25,11 @@ def _u32(t):
 
 
 def _last_split(native):
-    """{long spans, segments, overflow flag, quad-listed spans} of this thread's
-    last descriptor batch (test hook prismdb_crc32c_last_split)."""
+    """{long spans, segments, overflow flag, lane-listed spans} of this thread's
+    last planner-path descriptor batch (test hook prismdb_crc32c_last_split)."""
     import ctypes
 
     arr = (ctypes.c_uint64 * 4)()
-    native.prismdb_crc32c_last_split.argtypes = [ctypes.c_void_p]
-    native.prismdb_crc32c_last_split.restype = ctypes.c_int
     assert native.prismdb_crc32c_last_split(arr) == 0
     return list(arr)
 
@@ -42,7 +40,7 @@ def _to_dev(arr, dev):
     return torch.from_numpy(np.array(arr, copy=True)).to(dev)
 
 
-def test_golden_sweep_device(dev, golden):
+def test_golden_sweep_device(dev, golden, route):
     """Every reference golden vector (lengths 0..130 at offsets 0..7, block-sized
     spans, adversarial random spans, non-zero init) through batch()."""
     from prismdb_amd import crc32c
@@ -58,7 +56,7 @@ def test_golden_sweep_device(dev, golden):
     assert (_u32(outm) == rows[:, 4].astype(np.uint32)).all()
 
 
-def test_kats_device(dev, golden):
+def test_kats_device(dev, golden, route):
     from prismdb_amd import crc32c
 
     vecs = golden["kat"]["vectors"]
@@ -74,7 +72,7 @@ def test_kats_device(dev, golden):
     assert crc32c.as_u32(out) == [v["value"] for v in vecs]
 
 
-def test_long_stream_vectors_device(dev, golden):
+def test_long_stream_vectors_device(dev, golden, route):
     """Index-block sized spans (486 977 B), 1 MiB span: the split + combine path."""
     import torch
     from prismdb_amd import crc32c
@@ -150,7 +148,7 @@ def _check_spans(dev, oracle, host, off, lens, init=None, mask=False):
     np.testing.assert_array_equal(_u32(out), want)
 
 
-def test_mixed_sizes_config3(dev, oracle):
+def test_mixed_sizes_config3(dev, oracle, route):
     """Config-3 shape: lengths uniform over {1,4,16,64} KiB packed back to back."""
     rng = np.random.default_rng(0x5EED0003)
     lens = rng.choice([1024, 4096, 16384, 65536], size=3000).astype(np.uint64)
@@ -159,7 +157,7 @@ def test_mixed_sizes_config3(dev, oracle):
     _check_spans(dev, oracle, host, off, lens)
 
 
-def test_sst_shaped_config(dev, oracle):
+def test_sst_shaped_config(dev, oracle, route):
     """SST-shaped: 3988-B spans at stride 3992 plus one 486 977-B index span."""
     n = 2000
     off = [i * 3992 for i in range(n)] + [n * 3992]
@@ -168,7 +166,7 @@ def test_sst_shaped_config(dev, oracle):
     _check_spans(dev, oracle, host, off, lens, mask=True)
 
 
-def test_adversarial_random_spans(dev, oracle):
+def test_adversarial_random_spans(dev, oracle, route):
     """Random lengths 0..70 000 at random byte offsets, random init (overlapping allowed)."""
     rng = np.random.default_rng(0x5EED0007)
     size = 8 << 20
@@ -180,7 +178,7 @@ def test_adversarial_random_spans(dev, oracle):
     _check_spans(dev, oracle, host, off, lens, init)
 
 
-def test_tiny_and_empty_spans(dev, oracle):
+def test_tiny_and_empty_spans(dev, oracle, route):
     host = oracle.synth(1 << 16, 0x5EED0008)
     off, lens = [], []
     for n in range(0, 40):
@@ -190,7 +188,7 @@ def test_tiny_and_empty_spans(dev, oracle):
     _check_spans(dev, oracle, host, off, lens, init=[(i * 2654435761) & 0xFFFFFFFF for i in range(len(off))])
 
 
-def test_huge_span_split_path(dev, oracle):
+def test_huge_span_split_path(dev, oracle, route):
     """A 40 MiB span at an odd offset (1281 segments) and neighbours."""
     size = (40 << 20) + 4096
     host = oracle.synth(size, 0x5EED0009)
@@ -232,7 +230,7 @@ def test_pair_run_schedule(dev, oracle, native, n):
     np.testing.assert_array_equal(_u32(out2), oracle.batch(host, off, lens.astype(np.uint32))[0])
 
 
-def test_max_length_span(dev, oracle, native):
+def test_max_length_span(dev, oracle, native, route):
     """The longest span a descriptor holds (len = 2^32 - 1) at an odd offset,
     with an initial value, Mask and VERIFY against its stored trailer, next to
     a short span with a damaged trailer: the split path's 131 072 segments and
@@ -268,7 +266,8 @@ def test_max_length_span(dev, oracle, native):
     out, mm = crc32c.batch(buf, d_off, d_len, d_init, mask=True, verify=True)
     np.testing.assert_array_equal(_u32(out), want)
     assert mm.cpu().numpy().tolist() == [0, 1]
-    assert _last_split(native)[:3] == [1, 131072, 0]  # one long span, 2^17 segments, no overflow
+    if route == "lane_log":
+        assert _last_split(native)[:3] == [1, 131072, 0]  # one long span, 2^17 segments, no overflow
     out2, _ = crc32c.batch(buf, d_off[:1], d_len[:1], d_init[:1])  # unmasked, no verify
     assert int(_u32(out2)[0]) == int(raw[0])
     del buf, out, mm, out2
@@ -337,7 +336,7 @@ def test_long_spans_close_slices(dev, oracle, uniform):
     _check_spans(dev, oracle, host, off, lens, init, mask=True)
 
 
-def test_log_header_padding_skip(dev, oracle):
+def test_log_header_padding_skip(dev, oracle, route):
     """LOG_HEADER batches run the span kernel that skips chunk 0's padding
     rounds: short records paired with multi-chunk ones, empty and 1-3 byte
     records, random offsets; CRCs and the verify flags against the oracle
@@ -377,7 +376,7 @@ def test_log_header_padding_skip(dev, oracle):
 
 
 @pytest.mark.parametrize("n", [1, 7, 640, 5000])
-def test_slices_with_empty_slices(dev, oracle, n):
+def test_slices_with_empty_slices(dev, oracle, n, route):
     """Small batches of multi-task spans: the slice size drops to 1-2 tasks, so
     a 32-task span opens many empty slices that streams must step over."""
     rng = np.random.default_rng(0x5EED0012 + n)
@@ -388,7 +387,7 @@ def test_slices_with_empty_slices(dev, oracle, n):
     _check_spans(dev, oracle, host, off, lens)
 
 
-def test_verify_sst_fixture(dev, golden):
+def test_verify_sst_fixture(dev, golden, route):
     """ReadBlock verify semantics on the reference-built SST, clean and corrupted."""
     import torch
     from prismdb_amd import crc32c
@@ -689,23 +688,23 @@ def test_host_pipeline_failure_drains_ring(dev, oracle):
     np.testing.assert_array_equal(got, want)
 
 
-@pytest.fixture()
-def quad_all(native):
-    """Every descriptor batch through the quad kernel (prismdb_crc32c_quad_mode(1))."""
-    import ctypes
+@pytest.fixture(params=["lane_all", "direct"])
+def short_route(request, native):
+    """Short records through the lane kernel (every planner batch) and through
+    the one-launch kernel."""
+    from conftest import set_route
 
-    native.prismdb_crc32c_quad_mode.argtypes = [ctypes.c_int]
-    native.prismdb_crc32c_quad_mode(1)
-    yield
-    native.prismdb_crc32c_quad_mode(0)
+    restore = set_route(native, request.param)
+    yield request.param
+    restore()
 
 
 @pytest.mark.parametrize("log_header", [False, True])
-def test_quad_short_records(dev, oracle, quad_all, log_header):
-    """The short-record kernel on every length 0..1280 at every alignment, the
-    lengths just above its limit (generic path), random init, verify with the
-    stored crc after the span or (log records) 6 bytes before it, one damaged
-    record in four; record counts that end mid-task and mid-run."""
+def test_short_records(dev, oracle, short_route, log_header):
+    """Short records on every length 0..1280 at every alignment, the lengths
+    just above the lane kernel's limit (its generic path), random init, verify
+    with the stored crc after the span or (log records) 6 bytes before it, one
+    damaged record in four; record counts that end mid-run."""
     import torch
     from prismdb_amd import crc32c
 
@@ -737,9 +736,9 @@ def test_quad_short_records(dev, oracle, quad_all, log_header):
     np.testing.assert_array_equal(_u32(out2), oracle.batch(host, off, lens)[0])
 
 
-def test_quad_task_window(dev, oracle, quad_all):
-    """Records of one four-record task more than 2 GiB apart: the ones outside
-    the task's window go to the generic path, the results are the same."""
+def test_short_records_far_apart(dev, oracle, short_route):
+    """Neighbouring records more than 2 GiB apart (64-bit addresses in the
+    lane kernel's runs and the one-launch kernel's static runs)."""
     import torch
     from prismdb_amd import crc32c
 

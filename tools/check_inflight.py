@@ -155,8 +155,15 @@ def cstep(consts, t):
         c = {k: v for k, v in c.items() if not (sregs(k) & sregs(dst))}
         c[dst] = int(ops[1])
         return c
-    if op == "s_xor_b64" and len(ops) == 3 and ops[0] == ops[1] and ops[2] == "-1" and ops[0] in c:
-        c[ops[0]] = ~c[ops[0]]
+    if op == "s_xor_b64" and len(ops) == 3 and ops[2] == "-1" and ops[1] in c:
+        v = ~c[ops[1]]
+        c = {k: x for k, x in c.items() if not (sregs(k) & sregs(ops[0]))}
+        c[ops[0]] = v
+        return c
+    if op == "s_mov_b64" and len(ops) == 2 and ops[1] in c:
+        v = c[ops[1]]
+        c = {k: x for k, x in c.items() if not (sregs(k) & sregs(ops[0]))}
+        c[ops[0]] = v
         return c
     if op in ("s_andn2_b64", "s_and_b64") and len(ops) == 3 and ops[0] == "vcc" and ops[1] == "exec":
         x = c.get(ops[2])
