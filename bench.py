@@ -20,6 +20,12 @@ Printed (rank 0): ONE JSON line with the driver's contract fields plus
                 oracle/_ref/) on this host's cores over a bounded sample of the
                 same blocks, also cross-checked bit for bit against the GPU results
   e2e           (with --e2e) host-resident rate incl. pinned H2D/D2H copies
+  config5_partitions
+                BASELINE configs[4]: each rank one PrismDB partition of ~2.4 M
+                SST block spans (143 files), sealed and verified file by file
+                through the descriptor path, results gathered to rank 0 over
+                RCCL (N > 1); its own GiB/s, never the headline value
+                (--no-config5 skips it)
 """
 from __future__ import annotations
 
@@ -53,15 +59,35 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-seconds of reference work")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--e2e", action="store_true", help="also measure the host-resident (pinned copy) rate")
+    ap.add_argument("--no-config5", action="store_true", help="skip the config-5 partition leg")
+    ap.add_argument("--c5-spans", type=int, default=2_400_000, help="config-5 spans per partition (GPU)")
+    ap.add_argument("--c5-steps", type=int, default=5)
     return ap.parse_args()
 
 
+def affinity() -> list:
+    return sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else list(range(os.cpu_count() or 1))
+
+
 def cpu_threads() -> int:
-    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    """Threads for the CPU baseline: the cores this process may run on,
+    bounded by OMP_NUM_THREADS (16 on the GPU box: its share of the host)."""
+    n = len(affinity())
     env = os.environ.get("OMP_NUM_THREADS")
     if env and env.isdigit():
         n = min(n, int(env))
-    return max(1, min(n, 16))
+    return max(1, n)
+
+
+def _ranges(cpus: list) -> str:
+    out, i = [], 0
+    while i < len(cpus):
+        j = i
+        while j + 1 < len(cpus) and cpus[j + 1] == cpus[j] + 1:
+            j += 1
+        out.append(f"{cpus[i]}-{cpus[j]}" if j > i else f"{cpus[i]}")
+        i = j + 1
+    return ",".join(out)
 
 
 def cpu_model() -> str:
@@ -102,6 +128,11 @@ def cpu_baseline_leg(args, gpu_out) -> dict | None:
         def run(t, p):
             return lib.ref_crc32c_time_blocks(host.ctypes.data, BLOCK, BLOCK, nblk, t, p, out.ctypes.data)
     else:
+        # oracle/_ref/ (the reference compiled from /root/reference, shipped
+        # with the snapshot) is missing: time the C restatement instead, and
+        # say so in the line (kind "port", a warning on stderr)
+        print("warning: oracle/_ref/libref_crc32c.so is missing; cpu_baseline times the oracle port (kind=port)",
+              file=sys.stderr)
         kind = "port"
         accel = 0
         ora.oracle_crc32c_batch_fixed.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t,
@@ -122,8 +153,14 @@ def cpu_baseline_leg(args, gpu_out) -> dict | None:
     rate = nblk * BLOCK * passes / tn / GIB
     g = gpu_out[:nblk].cpu().numpy().view(np.uint32)
     agree = int((g == out).sum())
+    cpus = affinity()
     return {
         "value": round(rate, 3), "unit": "GiB/s", "cores": threads, "kind": kind,
+        "host_cores_total": os.cpu_count(),
+        "affinity": {"count": len(cpus), "cpus": _ranges(cpus)},
+        "kind_note": ("the reference's util/crc32c.cc compiled from /root/reference (oracle/_ref/)"
+                      if kind == "reference" else
+                      "PORT: oracle/_ref/ missing -- the oracle's C restatement on 1 thread, not the reference"),
         "sample": (f"crc32c::Value over the first {nblk} x 4096 B blocks of the same splitmix64 stream "
                    f"(host-resident, {nblk * BLOCK / GIB:.2f} GiB), {passes} passes on {threads} threads "
                    f"(~{tn * threads:.1f} CPU-s); 1 thread: {rate1:.3f} GiB/s"),
@@ -145,7 +182,7 @@ def load_pmc_traffic(nblocks: int):
         except (OSError, ValueError):
             continue
         if d.get("nblocks") == nblocks and d.get("hbm_bytes_per_launch"):
-            best = d
+            best = dict(d, _path=os.path.relpath(p, ROOT))
     return best
 
 
@@ -252,6 +289,123 @@ def compaction_leg(torch, crc32c, dev, nfiles: int = 115) -> dict:
     return res
 
 
+C5_ND, C5_DATA, C5_STRIDE, C5_INDEX = 16811, 3988, 3992, 486977  # one 64 MiB SST
+
+
+def config5_leg(args, torch, dist, crc32c, dev, rank, world) -> dict:
+    """BASELINE configs[4] (scripts/config_test_100gb.yml): 8 partitions, ~19.3 M
+    block spans, partition p on GPU p -- ~2.4 M spans per GPU, here as the SST
+    files that partition's compactions write: nfiles x (16 811 data spans of
+    contents||type = 3988 B at stride 3992 + one 486 977-B index span), device-
+    resident.  One step = every file of the partition through one
+    leveldb_crc32c_batch call each (the granularity PrismDB calls at:
+    TableBuilder::Finish seals a file, table/table_builder.cc:185-261; a
+    compaction verifies its inputs block by block, table/format.cc:91-102),
+    then (N > 1) one RCCL gather of the partition's 4-byte results to rank 0.
+    Seal = MASK | WRITE_TRAILER (trailers written in place), verify = the
+    mismatch vector.  GiB/s of span bytes, whole job (all ranks), max-over-
+    ranks timing between barriers.  Checks: verify after seal flags nothing
+    and returns the unmasked seal results; 256 spans of file 0 against the
+    host leveldb_crc32c_value; the gathered digests."""
+    import numpy as np
+    from prismdb_amd._lib import lib
+    from prismdb_amd.dist import ShardedBatch
+
+    spf = C5_ND + 1
+    nfiles = -(-args.c5_spans // spf)
+    fbytes = (C5_ND * C5_STRIDE + C5_INDEX + 4 + 255) & ~255
+    span_bytes = C5_ND * C5_DATA + C5_INDEX
+    buf = torch.empty(nfiles * fbytes, dtype=torch.uint8, device=dev)
+    crc32c.fill_synthetic(buf, SEED ^ 0xC5C5, byte_offset=rank * nfiles * fbytes)
+    off1 = np.concatenate([np.arange(C5_ND, dtype=np.int64) * C5_STRIDE, [C5_ND * C5_STRIDE]])
+    len1 = np.concatenate([np.full(C5_ND, C5_DATA, dtype=np.int64), [C5_INDEX]])
+    typ = (np.arange(nfiles, dtype=np.int64)[:, None] * fbytes + (off1 + len1 - 1)[None, :]).reshape(-1)
+    buf[torch.from_numpy(typ).to(dev)] = 0  # type byte kNoCompression
+    d_off = torch.from_numpy(off1).to(dev)
+    d_len = torch.from_numpy(len1.astype(np.int32)).to(dev)
+    n = nfiles * spf
+    out = torch.empty(n, dtype=torch.int32, device=dev)
+    raw = torch.empty(n, dtype=torch.int32, device=dev)
+    mm = torch.empty(n, dtype=torch.uint8, device=dev)
+    L = lib()
+    stream = torch.cuda.current_stream()
+    sp = int(stream.cuda_stream)
+    base, op, lp = buf.data_ptr(), d_off.data_ptr(), d_len.data_ptr()
+
+    def run(verify):
+        o = raw.data_ptr() if verify else out.data_ptr()
+        for f in range(nfiles):
+            rc = L.leveldb_crc32c_batch(base + f * fbytes, op, lp, None, spf, o + 4 * f * spf,
+                                        (mm.data_ptr() + f * spf) if verify else None,
+                                        0 if verify else 0x3, sp)  # seal: MASK | WRITE_TRAILER
+            if rc != 0:
+                raise RuntimeError(f"leveldb_crc32c_batch: {L.leveldb_crc32c_last_error().decode()}")
+
+    shard = ShardedBatch(nblocks_per_rank=n, block_bytes=0, rank=rank, world=world, device=dev, slots=1) \
+        if world > 1 else None
+
+    def leg(verify):
+        res = out if not verify else raw
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(args.c5_steps)]
+        for _ in range(2):
+            run(verify)
+            if shard:
+                shard.gather_async(res, 0).wait()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(args.c5_steps):
+            ev[i][0].record(stream)
+            run(verify)
+            ev[i][1].record(stream)
+            if shard:
+                shard.gather_async(res, 0).wait()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        kern = sum(a.elapsed_time(b) for a, b in ev) / args.c5_steps
+        t = torch.tensor([el, kern], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el, kern = float(t[0]), float(t[1])
+        d = {"value": round(world * nfiles * span_bytes * args.c5_steps / el / GIB, 2), "unit": "GiB/s",
+             "ms_per_step": round(el * 1e3 / args.c5_steps, 3),
+             "batch_ms_per_step_max_rank": round(kern, 3),
+             "us_per_file_call": round(kern * 1e3 / nfiles, 2)}
+        if shard:
+            d["gather_check"] = shard.check_gathered(res, 0)
+        return d
+
+    seal = leg(False)
+    verify = leg(True)
+    torch.cuda.synchronize()
+    bad = int(mm.sum().item())
+    unmasked = (out.to(torch.int64) & 0xFFFFFFFF) - 0xA282EAD8
+    unmasked = unmasked & 0xFFFFFFFF
+    unmasked = ((unmasked >> 17) | (unmasked << 15)) & 0xFFFFFFFF  # Unmask (util/crc32c.h:34-37)
+    same = bool(torch.equal(unmasked, raw.to(torch.int64) & 0xFFFFFFFF))
+    host0 = buf[:fbytes].cpu().numpy()
+    pick = np.random.default_rng(rank).choice(spf, size=min(256, spf), replace=False)
+    r0 = raw[:spf].cpu().numpy().view(np.uint32)
+    host_ok = all(crc32c.Value(host0[off1[i]:off1[i] + len1[i]].tobytes()) == int(r0[i]) for i in pick)
+    del buf, out, raw, mm
+    return {
+        "workload": (f"config5: partition {rank} of {world} on GPU {rank}: {nfiles} SST files x ({C5_ND} x "
+                     f"{C5_DATA} B @ {C5_STRIDE} + 1 x {C5_INDEX} B) = {n} spans per GPU, one "
+                     "leveldb_crc32c_batch per file" + (", RCCL gather of the results to rank 0" if world > 1 else "")),
+        "files_per_gpu": nfiles, "spans_per_gpu": n, "span_bytes_per_gpu": nfiles * span_bytes,
+        "steps": args.c5_steps, "scaling": "weak",
+        "seal": seal, "verify": verify,
+        "checks": {"verify_after_seal_mismatches": bad, "verify_equals_unmasked_seal": same,
+                   "host_value_256_spans_file0": host_ok},
+    }
+
+
 def main() -> int:
     args = parse()
     import torch
@@ -343,6 +497,11 @@ def main() -> int:
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline_leg(args, outs[(args.steps - 1) % 2])
     e2e = e2e_leg(args, torch, crc32c, dev) if (args.e2e and rank == 0 and world == 1) else None
+    c5 = None
+    if not args.no_config5:
+        del buf  # the config-2 blocks; the results stay for the checks above
+        torch.cuda.empty_cache()
+        c5 = config5_leg(args, torch, dist, crc32c, dev, rank, world)
 
     if rank == 0:
         pmc = load_pmc_traffic(nblk)
@@ -376,6 +535,9 @@ def main() -> int:
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": pmc["hbm_bytes_per_launch"] if pmc else None,
+                "traffic_source": (f"{pmc['_path']}: committed rocprofv3 --pmc run of this workload "
+                                   "(FETCH_SIZE + WRITE_SIZE per launch, gfx950-corrected), not measured in this run"
+                                   if pmc else None),
                 "kernel": "crc32c_fixed_kernel<16, false>",
                 "kernel_ms": round(kern_ms, 4),
                 "kernel_ms_max_rank": round(kern_ms_max, 4),
@@ -387,6 +549,8 @@ def main() -> int:
             line["gather_check"] = gathered_ok
         if e2e is not None:
             line["e2e_host_resident"] = e2e
+        if c5 is not None:
+            line["config5_partitions"] = c5
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()

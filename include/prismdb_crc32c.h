@@ -115,6 +115,26 @@ int leveldb_crc32c_batch_host(const void* host_base, const uint64_t* off, const 
                               const uint32_t* init, size_t n, uint32_t* out, uint8_t* mismatch,
                               uint32_t flags);
 
+/*
+ * Several devices from one process: PrismDB's partitions (db/db_impl.h:359,
+ * one background thread each, util/env_posix.cc:850-890) with partition p's
+ * blocks resident on device devices[p].  Each device checksums its batch
+ * (span i of partition p = dev_base[p][dev_off[p][i], + dev_len[p][i]),
+ * dev_init may be NULL, dev_init[p] may be NULL), then one RCCL gather over
+ * xGMI (grouped ncclSend/ncclRecv, communicators from ncclCommInitAll, kept
+ * per device list) brings the results to devices[0]: out0 / mismatch0 are
+ * device arrays on devices[0] of n[0] + ... + n[ndev-1] entries, partition
+ * after partition (either may be NULL, not both).  flags as for
+ * leveldb_crc32c_batch (WRITE_TRAILER seals in place on every device).
+ * streams may be NULL (null streams) or hold one stream per device: the work
+ * is ordered after what is already on streams[p] and streams[p] waits for
+ * it.  Calls with the same device list are serialized.
+ */
+int leveldb_crc32c_batch_multi(int ndev, const int* devices, const void* const* dev_base,
+                               const uint64_t* const* dev_off, const uint32_t* const* dev_len,
+                               const uint32_t* const* dev_init, const size_t* n, uint32_t* out0,
+                               uint8_t* mismatch0, uint32_t flags, void* const* streams);
+
 /* Thread-local message for the last non-zero return on this thread. */
 const char* leveldb_crc32c_last_error(void);
 

@@ -19,7 +19,7 @@ extern "C" {
 #define PRISMDB_SST_ECORRUPT (-10)  /* message: the reference's Status text */
 #define PRISMDB_SST_ECAPACITY (-11) /* *n_out holds the count needed */
 #define PRISMDB_SST_EUNSUPPORTED (-12) /* "Not implemented: ...": a snappy-compressed
-                                          index or metaindex block */
+                                          index block */
 
 /* block kinds */
 #define PRISMDB_SST_DATA 0
@@ -39,8 +39,11 @@ extern "C" {
  *
  * Limit: the walker does not decompress.  Tables written with
  * Options::compression = kSnappyCompression (table/table_builder.cc:159) may
- * hold a snappy index or metaindex block; those return
- * PRISMDB_SST_EUNSUPPORTED instead of a misparse.  Snappy *data* blocks are
+ * hold a snappy index block; that returns PRISMDB_SST_EUNSUPPORTED instead
+ * of a misparse.  A snappy (or any other non-raw type) metaindex is not
+ * walked -- no filter span is listed -- but is still listed itself and so
+ * verified by the batch; the reference ignores metaindex errors too
+ * (Table::ReadMeta, table/table.cc:84-111).  Snappy *data* blocks are
  * fine: their checksum covers the stored (compressed) bytes.  PrismDB's
  * default is kNoCompression (include/leveldb/options.h:134).
  *

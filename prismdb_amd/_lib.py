@@ -28,6 +28,7 @@ C_ABI_SYMBOLS = (
     "leveldb_crc32c_batch_fixed",
     "leveldb_crc32c_batch",
     "leveldb_crc32c_batch_host",
+    "leveldb_crc32c_batch_multi",
     "leveldb_crc32c_last_error",
     "prismdb_fill_synthetic",
     "leveldb_sst_block_spans",
@@ -60,6 +61,7 @@ def _declare(lib: ctypes.CDLL) -> None:
         "leveldb_crc32c_batch_fixed": (ctypes.c_int, [vp, sz, sz, sz, u32, vp, vp, u32, vp]),
         "leveldb_crc32c_batch": (ctypes.c_int, [vp, vp, vp, vp, sz, vp, vp, u32, vp]),
         "leveldb_crc32c_batch_host": (ctypes.c_int, [vp, vp, vp, vp, sz, vp, vp, u32]),
+        "leveldb_crc32c_batch_multi": (ctypes.c_int, [ctypes.c_int, vp, vp, vp, vp, vp, vp, vp, vp, u32, vp]),
         "leveldb_crc32c_last_error": (ctypes.c_char_p, []),
         "prismdb_fill_synthetic": (ctypes.c_int, [vp, sz, u64, u64, vp]),
         "prismdb_crc32c_extend_portable": (u32, [u32, cp, sz]),

@@ -25,7 +25,7 @@ OBJDIR = os.path.join(ROOT, "build", "obj")
 LIB = os.path.join(LIBDIR, "libprismdb_crc32c.so")
 
 ARCH = os.environ.get("PRISMDB_OFFLOAD_ARCH", "gfx950")
-HIP_SOURCES = ["crc32c_kernels.hip", "crc32c_direct.hip", "crc32c_capi.hip", "crc32c_pipeline.hip", "synth.hip"]
+HIP_SOURCES = ["crc32c_kernels.hip", "crc32c_direct.hip", "crc32c_capi.hip", "crc32c_multi.hip", "crc32c_pipeline.hip", "synth.hip"]
 CXX_SOURCES = ["crc32c_host.cc", "sst.cc", "log_reader.cc"]
 HEADERS = ["crc32c_device.h", "crc32c_gf2.h", "crc32c_fold.h"]
 
@@ -89,7 +89,7 @@ def build(force: bool = False, asm: bool = False, verbose: bool = False, defines
     exports = os.path.join(CSRC, "exports.map")
     if force or jobs or _stale(lib_out, objs + [exports]):
         _run([hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", f"-Wl,--version-script={exports}",
-              "-o", lib_out, *objs])
+              "-o", lib_out, *objs, "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"])
     if asm:
         asmdir = os.path.join(ROOT, "build", "asm")
         os.makedirs(asmdir, exist_ok=True)

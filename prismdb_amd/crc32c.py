@@ -10,6 +10,8 @@ native library's leveldb::crc32c::Extend.
 Batch surface (device-resident spans, one call = one batch of SST blocks):
     batch_fixed(buf, stride, length, nblocks, ...)   block i = buf[i*stride : i*stride+length]
     batch(buf, off, lens, init=None, ...)            span i  = buf[off[i] : off[i]+lens[i]]
+    batch_multi([(buf, off, lens), ...], ...)        one partition per device, results gathered
+                                                     to the first partition's device (RCCL)
 buf/off/lens/init/out are torch tensors on the current HIP device; calls are
 enqueued on torch's current stream.  mask=True applies Mask() to each result
 (TableBuilder::WriteRawBlock, table/table_builder.cc:194-196); verify=True also
@@ -20,6 +22,7 @@ Status::Corruption("block checksum mismatch"), see prismdb_amd.sst.
 """
 from __future__ import annotations
 
+import ctypes
 from contextlib import nullcontext as _nullcontext
 from typing import Optional, Tuple
 
@@ -129,8 +132,10 @@ def batch(buf, off, lens, init=None, *, mask: bool = False, verify: bool = False
 
     check_bounds: every span, with its stored trailer or log header, must lie
     inside buf (ValueError otherwise; a bad descriptor would be a device
-    fault).  The check is one device reduction and a host sync; callers that
-    reuse descriptors they have already checked may pass False."""
+    fault).  The check is one device reduction and a host sync, so with the
+    default the call blocks the host even when `stream` is given; callers
+    that reuse descriptors they have already checked pass False and stay
+    asynchronous."""
     if trailer and verify:
         raise ValueError("trailer and verify are exclusive")
     torch = _torch()
@@ -145,8 +150,10 @@ def batch(buf, off, lens, init=None, *, mask: bool = False, verify: bool = False
         lead, tail = _span_reach(log_header, verify, trailer)
         with torch.cuda.stream(stream) if stream is not None else _nullcontext():
             end = off + (lens.to(torch.int64) & 0xFFFFFFFF)
-            lo, hi = torch.stack([off.min(), end.max()]).tolist()
-        if lo < lead or hi + tail > buf.numel() * buf.element_size():
+            lo, omax, hi = torch.stack([off.min(), off.max(), end.max()]).tolist()
+        # 0 <= off <= size for every span first: then no off + len wraps
+        size = buf.numel() * buf.element_size()
+        if lo < lead or omax > size or hi + tail > size:
             raise ValueError(f"spans reach [{lo - lead}, {hi + tail}) outside buf "
                              f"({buf.numel() * buf.element_size()} bytes)")
     init = init.contiguous() if init is not None else None
@@ -163,6 +170,80 @@ def batch(buf, off, lens, init=None, *, mask: bool = False, verify: bool = False
     return out, (mismatch if verify else None)
 
 
+def batch_multi(parts, *, mask: bool = False, verify: bool = False, trailer: bool = False,
+                log_header: bool = False, out=None, mismatch=None, streams=None, check_bounds: bool = True):
+    """Partitions on several devices from one process
+    (leveldb_crc32c_batch_multi): parts[p] = (buf, off, lens[, init]) device
+    tensors on one device each (distinct devices; parts[0]'s is the root).
+    Every device checksums its partition, and an RCCL gather brings the
+    results to the root device, partition after partition.
+
+    Returns (out int32 tensor [sum n] on the root device, mismatch uint8 or
+    None).  streams: None (each device's current stream) or one torch stream
+    per part."""
+    torch = _torch()
+    if trailer and verify:
+        raise ValueError("trailer and verify are exclusive")
+    if not parts:
+        raise ValueError("batch_multi needs at least one partition")
+    ndev = len(parts)
+    devs, bases, offs, lns, inits, ns = [], [], [], [], [], []
+    for p, part in enumerate(parts):
+        buf, off, lens = part[0], part[1], part[2]
+        init = part[3] if len(part) > 3 else None
+        _require_device(buf, off, lens, init)
+        d = buf.device.index
+        for t in (off, lens, init):
+            if t is not None and t.device != buf.device:
+                raise ValueError(f"partition {p}: its tensors must be on one device")
+        if off.dtype != torch.int64 or lens.dtype != torch.int32 or (init is not None and init.dtype != torch.int32):
+            raise TypeError("off must be int64, lens/init int32 (uint32 bit patterns)")
+        n = off.numel()
+        if lens.numel() != n or (init is not None and init.numel() != n):
+            raise ValueError(f"partition {p}: off, lens and init must have the same length")
+        off, lens = off.contiguous(), lens.contiguous()
+        init = init.contiguous() if init is not None else None
+        if check_bounds and n:
+            lead, tail = _span_reach(log_header, verify, trailer)
+            with torch.cuda.device(d):
+                end = off + (lens.to(torch.int64) & 0xFFFFFFFF)
+                lo, omax, hi = torch.stack([off.min(), off.max(), end.max()]).tolist()
+            size = buf.numel() * buf.element_size()
+            if lo < lead or omax > size or hi + tail > size:
+                raise ValueError(f"partition {p}: spans reach [{lo - lead}, {hi + tail}) outside its buffer")
+        devs.append(d)
+        bases.append(buf.data_ptr())
+        offs.append(off)
+        lns.append(lens)
+        inits.append(init)
+        ns.append(n)
+    if len(set(devs)) != ndev:
+        raise ValueError("batch_multi: one partition per device")
+    total = sum(ns)
+    root = torch.device("cuda", devs[0])
+    if out is None:
+        out = torch.empty(total, dtype=torch.int32, device=root)
+    if verify and mismatch is None:
+        mismatch = torch.empty(total, dtype=torch.uint8, device=root)
+    P = ctypes.c_void_p * ndev
+    c_dev = (ctypes.c_int * ndev)(*devs)
+    c_base = P(*bases)
+    c_off = P(*[t.data_ptr() for t in offs])
+    c_len = P(*[t.data_ptr() for t in lns])
+    c_init = P(*[t.data_ptr() if t is not None else None for t in inits])
+    c_n = (ctypes.c_size_t * ndev)(*ns)
+    if streams is None:
+        streams = [torch.cuda.current_stream(d) for d in devs]
+    c_st = P(*[int(s.cuda_stream) for s in streams])
+    flags = (FLAG_MASK if mask else 0) | (FLAG_WRITE_TRAILER if trailer else 0) | (FLAG_LOG_HEADER if log_header else 0)
+    keep = (offs, lns, inits)  # alive until the call has enqueued its work  # noqa: F841
+    rc = lib().leveldb_crc32c_batch_multi(ndev, c_dev, c_base, c_off, c_len,
+                                          c_init if any(t is not None for t in inits) else None, c_n,
+                                          out.data_ptr(), mismatch.data_ptr() if verify else None, flags, c_st)
+    check(rc, "leveldb_crc32c_batch_multi")
+    return out, (mismatch if verify else None)
+
+
 def batch_host(base, off, lens, init=None, *, mask: bool = False, verify: bool = False, log_header: bool = False):
     """Host-resident batch: numpy (or pinned torch CPU tensor) buffer and
     descriptors in host memory; streamed through the device by the engine.
@@ -170,6 +251,9 @@ def batch_host(base, off, lens, init=None, *, mask: bool = False, verify: bool =
     import numpy as np
 
     n = len(off)
+    off = np.asarray(off)
+    if n and off.dtype.kind == "i" and int(off.min()) < 0:  # before the cast: -1 would wrap to 2^64 - 1
+        raise ValueError("negative span offset")
     off = np.ascontiguousarray(off, dtype=np.uint64)
     lens = np.ascontiguousarray(lens, dtype=np.uint32)
     ini = np.ascontiguousarray(init, dtype=np.uint32) if init is not None else None
@@ -178,8 +262,10 @@ def batch_host(base, off, lens, init=None, *, mask: bool = False, verify: bool =
     nbytes = base.numel() * base.element_size() if hasattr(base, "data_ptr") else base.nbytes
     if n:
         lead, tail = _span_reach(log_header, verify, False)
-        lo, hi = int(off.min()), int((off + lens.astype(np.uint64)).max())
-        if lo < lead or hi + tail > nbytes:
+        lo, omax = int(off.min()), int(off.max())
+        # 0 <= off <= nbytes for every span first: then no off + len wraps
+        hi = int((off + lens.astype(np.uint64)).max()) if omax <= nbytes else omax
+        if lo < lead or omax > nbytes or hi + tail > nbytes:
             raise ValueError(f"spans reach [{lo - lead}, {hi + tail}) outside the host buffer ({nbytes} bytes)")
     out = np.empty(n, dtype=np.uint32)
     mm = np.empty(n, dtype=np.uint8) if verify else None

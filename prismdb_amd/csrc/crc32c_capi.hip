@@ -55,6 +55,7 @@ struct DeviceCtx {
   std::string error;
   DeviceTables* tabs = nullptr;
   int cus = 0;
+  hipStream_t release = nullptr;  // frees of released workspaces (non-blocking: waits for nothing else)
 };
 
 DeviceCtx g_ctx[kMaxDevices];
@@ -140,7 +141,7 @@ int SelfTest(DeviceCtx& ctx) {
   if (e == hipSuccess) e = hipMemcpy(d_len, len, sizeof(len), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemset(d_out, 0, sizeof(uint32_t) * 3);
   if (e != hipSuccess) {
-    hipFree(d);
+    (void)hipFree(d);
     delete[] h;
     return FailHip(e, "self-test upload");
   }
@@ -171,7 +172,7 @@ int SelfTest(DeviceCtx& ctx) {
       rc = Fail(PRISMDB_CRC32C_ESELFTEST, buf);
     }
   }
-  hipFree(d);
+  (void)hipFree(d);
   delete[] h;
   return rc;
 }
@@ -180,6 +181,12 @@ void InitDevice(DeviceCtx& ctx, int device) {
   hipError_t e = hipDeviceGetAttribute(&ctx.cus, hipDeviceAttributeMultiprocessorCount, device);
   if (e != hipSuccess || ctx.cus <= 0) {
     ctx.status = FailHip(e, "hipDeviceGetAttribute(multiprocessor count)");
+    ctx.error = t_last_error;
+    return;
+  }
+  e = hipStreamCreateWithFlags(&ctx.release, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    ctx.status = FailHip(e, "release stream");
     ctx.error = t_last_error;
     return;
   }
@@ -221,6 +228,7 @@ int GetCtx(DeviceCtx** out) {
 struct Workspace {
   int device = -1;
   hipStream_t stream = nullptr;
+  hipEvent_t done = nullptr;  // recorded on `stream` after every batch that used the workspace
   void* mem = nullptr;
   char* grow = nullptr;
   size_t cap_rec = 0;
@@ -232,29 +240,30 @@ struct Workspace {
 };
 
 // A thread that has used more streams than this evicts its least recently
-// used workspace (after synchronising that device: rare by construction).
+// used workspace.
 constexpr size_t kMaxWorkspaces = 8;
 
-// Every block of w, after the device has finished all work (callers
-// synchronise): stream-ordered frees on the null stream.
-void ReleaseWorkspace(Workspace& w) {
-  if (w.mem) (void)hipFree(w.mem);
-  if (w.grow) (void)hipFreeAsync(w.grow, nullptr);
-  if (w.qgrow) (void)hipFreeAsync(w.qgrow, nullptr);
-  if (w.direct) (void)hipFreeAsync(w.direct, nullptr);
-  (void)hipStreamSynchronize(nullptr);
-  w = Workspace{};
-}
-
+// Give w's device memory back: wait for the last batch that used it (its
+// event -- valid even when the caller has destroyed the stream; nothing
+// device-wide), free every block on the device's release stream, and trim
+// the default pool so the memory leaves the process's pool too.
 void SyncAndRelease(Workspace& w) {
   if (t_last_counters == w.ws.counters) t_last_counters = nullptr;
   if (w.direct != nullptr && t_last_stats == reinterpret_cast<const uint32_t*>(w.direct + 16)) t_last_stats = nullptr;
   int cur = 0;
   (void)hipGetDevice(&cur);
   if (w.device != cur) (void)hipSetDevice(w.device);
-  (void)hipDeviceSynchronize();
-  ReleaseWorkspace(w);
+  if (w.done != nullptr) (void)hipEventSynchronize(w.done);
+  const hipStream_t rs = g_ctx[w.device].release;
+  for (void* blk : {static_cast<void*>(w.mem), static_cast<void*>(w.grow), static_cast<void*>(w.qgrow),
+                    static_cast<void*>(w.direct)})
+    if (blk != nullptr) (void)hipFreeAsync(blk, rs);
+  (void)hipStreamSynchronize(rs);
+  hipMemPool_t pool = nullptr;
+  if (hipDeviceGetDefaultMemPool(&pool, w.device) == hipSuccess) (void)hipMemPoolTrimTo(pool, 0);
+  if (w.done != nullptr) (void)hipEventDestroy(w.done);
   if (w.device != cur) (void)hipSetDevice(cur);
+  w = Workspace{};
 }
 
 struct WorkspaceCache {
@@ -305,10 +314,12 @@ Workspace* FindWorkspace(hipStream_t s, int& rc) {
   w.stream = s;
   const size_t bytes = 256 + kCapSeg * (16 + 4) + (size_t)kCapLong * (8 + 8 + 4) +
                        (size_t)prismdb::dev::kMaxPlanBlocks * 8;
-  e = hipMalloc(&w.mem, bytes);
+  e = hipEventCreateWithFlags(&w.done, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipMallocAsync(&w.mem, bytes, s);
   if (e != hipSuccess) {
+    if (w.done != nullptr) (void)hipEventDestroy(w.done);
     lru.pop_front();
-    rc = FailHip(e, "workspace hipMalloc");
+    rc = FailHip(e, "workspace allocation");
     return nullptr;
   }
   char* p = static_cast<char*>(w.mem);
@@ -429,6 +440,12 @@ int RunBatch(DeviceCtx& ctx, const SpanBatch& base_args, bool desc, bool verify,
   int rc = 0;
   Workspace* w = FindWorkspace(s, rc);
   if (w == nullptr) return rc;
+  // whatever follows, the workspace's event marks the end of this call's work
+  struct MarkDone {
+    Workspace* w;
+    hipStream_t s;
+    ~MarkDone() { (void)hipEventRecord(w->done, s); }
+  } mark{w, s};
   const bool direct = desc && (route == kRouteDirect ||
                                (route == kRouteAuto && a.n <= g_direct_max.load(std::memory_order_relaxed)));
   if (direct && a.n <= prismdb::dev::kDirectMaxSpans &&
@@ -550,7 +567,7 @@ int leveldb_crc32c_device_init(int device) {
   }
   DeviceCtx* ctx = nullptr;
   int rc = GetCtx(&ctx);
-  if (device != cur) hipSetDevice(cur);
+  if (device != cur) (void)hipSetDevice(cur);
   return rc;
 }
 

@@ -145,7 +145,7 @@ struct SplitWs {
 // into tickets of 2^lg chunks that any wave may claim, and the wave that
 // finishes a span's last ticket combines the partial registers.
 constexpr uint64_t kDirectMaxSpans = 1ull << 17;
-constexpr int kDirectThreads = 512;  // per group, one group per CU: a wave's static run is <= 64 spans
+constexpr int kDirectThreads = 768;  // per group, one group per CU: a wave's static run is <= 64 spans
                                      // while n <= 64 * 8 * CUs (host-checked)
 constexpr uint32_t kDirectTickets = 1u << 20;  // ticket workspace (beyond it: whole spans, one wave each)
 constexpr uint32_t kNullSpan = 0xFFFFFFFFu;

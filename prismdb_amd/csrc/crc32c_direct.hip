@@ -6,40 +6,51 @@
 // are verified block by block (ReadBlock, table/format.cc:91-102).  The
 // planner path (crc32c_kernels.hip: memset, plan, slice scan and mark, span
 // pass, segment pass, combine) spends 5-7 launches of 4-6 us each on ~10 us of
-// data at that size.  This kernel does a file in one launch, 8 waves per CU:
+// data at that size.  This kernel does a file in one launch, 12 waves per CU
+// (one 768-thread group: the tables take all of LDS):
 //
-//   static run   wave w owns ~n / nwaves consecutive spans (<= 64; lane j
-//                holds span j's descriptor).  Its spans of one 4 KiB chunk
-//                (all the data blocks of an SST) go through an inline-asm
-//                ring of two slots x two streams -- the streams take
-//                alternate spans, so each fold reads two adjacent blocks, as
-//                the fixed kernel's pairs do -- with counted vmcnt waits and
-//                one coalesced store of the run's results.
-//   long spans   (more than one chunk) are found by their run's wave before
-//                anything else and cut into T tickets of g = 2^lg chunks (the
-//                smallest g <= 8 that gives T <= 64; the first ticket takes
-//                the remainder).  The wave pushes all its tickets with ONE
-//                64-bit atomic on word = supply << 32 | claimed and writes
-//                the ticket map (span, first ticket, T | lg, gen).
-//   tickets      every wave claims up to two tickets right after loading the
-//                tables (so a long span's chunks go out with the first loads
-//                and its combine is off the kernel's tail), and claims again,
-//                one at a time, after its static run until none is left.
+//   static run   wave w < K owns q or q + 1 consecutive spans (<= 64; lane j
+//                holds span j's descriptor).  Its one-chunk spans (all the
+//                data blocks of an SST) go through an inline-asm ring of two
+//                slots x three streams -- stream st takes run positions st,
+//                st + 3, ..., so a fold reads three neighbouring blocks --
+//                with counted vmcnt waits and one coalesced store of the
+//                run's results.  At 12 waves per CU an SST file's ~5.5 spans
+//                per wave are all requested at once.
+//   long spans   (more than one 4 KiB chunk) are found by their run's wave
+//                first and cut into T tickets of g = 2^lg chunks (the smallest
+//                g <= 8 that gives T <= 64; ticket 0 takes the remainder).  The
+//                wave pushes all its tickets with ONE 64-bit atomic on
+//                word = supply << 32 | claimed and writes the ticket map
+//                (span, first ticket, T | lg, gen -- gen last, release).
+//   workers      the last nwaves / 32 waves have no run (at most 256 of them:
+//                every worker reads `word`, and same-address reads serialize
+//                in one L2 channel, ~2.5 ns each).  A worker polls `word` for
+//                up to ~5 us, claims tickets one at a time while any are
+//                visible, and leaves.  A long span's chunks thus go out with
+//                the first loads instead of on the kernel's tail.
+//   late claims  a wave that pushed tickets claims, after its own run, one at
+//                a time until none is left, so every pushed ticket is claimed
+//                by someone.  Other static waves just leave (3072 reads of
+//                `word` at the end cost ~8 us).
 //
-// A claim is one atomicAdd of k on word: tickets [C, C + k) below the supply
-// S are the claimer's.  Tickets >= S were taken before they existed
-// ("orphans"): the wave that pushes them later sees claimed > its first ticket
-// and does those itself.  So no wave ever waits for another wave's progress,
-// except for a ticket-map entry that a running wave is writing (its push came
-// before the claim).  A ticket folds its chunks into a partial register R_k
-// (ticket 0 from the span's initial register, the others from 0) with plain
-// compiler-scheduled buffer loads; the wave that finishes a span's last ticket
-// (per-span counter) combines R = sum_k M^(T-1-k) R_k, M = shift_{4 KiB g},
-// lane-parallel as crc32c_combine_kernel does, feeds the tail bytes and stores
-// the results.  The last group to finish resets word and the group counter
-// for the next call on the stream (the workspace is per (thread, stream)).  If
-// the ticket workspace is full, the discovering wave folds its long spans
-// whole.
+// A claim is one atomicAdd of 1 on the claimed half of `word`: ticket C below
+// the supply S is the claimer's.  A claim at C >= S ("orphan": two workers
+// raced for the last visible ticket) belongs to whoever pushes ticket C: the
+// pusher sees claimed > its first ticket and folds those itself.  So no wave
+// waits for another wave's progress, except for a ticket-map entry that a
+// running wave is writing (its push came before the claim).  A ticket folds
+// its chunks into a partial register R_k (ticket 0 from the span's initial
+// register, the others from 0) with compiler-scheduled buffer loads; the wave
+// that finishes a span's last ticket (per-span counter) combines
+// R = sum_k M^(T-1-k) R_k, M = shift_{4 KiB g}, lane-parallel as
+// crc32c_combine_kernel does, feeds the tail bytes and stores the result.
+// The last group to finish resets `word` and the group counter for the next
+// call on the stream (the workspace is per (thread, device, stream)).  If the
+// ticket workspace is full, the discovering wave folds its long spans whole.
+// Test hooks (DirectWs::dbg): bit 0 delays every push by ~100 us, bit 1 makes
+// every worker claim once blindly (orphans); stats[] counts adopted tickets,
+// whole spans, worker claims and late claims.
 #include "crc32c_fold.h"
 
 namespace prismdb {
@@ -111,10 +122,10 @@ __device__ __forceinline__ DTask geometry(uint64_t p, uint32_t len) {
 
 }  // namespace
 
-// 8 waves per CU (one group: the tables take all of LDS): 256 VGPRs per lane
-// for the ring, the run's descriptors and the combine; 2048 waves keep
-// 8 tasks x 4 KiB in flight each, 64 MiB over the chip, which HBM needs far
-// less of (8 TB/s x ~2 us).
+// 12 waves per CU (one group: the tables take all of LDS), <= 168 VGPRs per lane
+// for the ring, the run's descriptors and the combine; 3072 waves keep six
+// tasks x 4 KiB in flight each, 72 MiB over the chip: a whole SST file's
+// reads are issued at once.
 constexpr uint32_t kDirectWaves = kDirectThreads / 64u;
 
 template <bool kVerify>
@@ -129,17 +140,25 @@ __global__ __launch_bounds__(kDirectThreads) void crc32c_direct_kernel(SpanBatch
   const uint64_t base = reinterpret_cast<uint64_t>(a.base);
   __shared__ uint32_t lds[kLdsWords];
 
-  // ---- the wave's static run: pairs [plo, phi) -> spans [sbase, sbase + m),
-  // m <= 64; lane j holds span sbase + j's descriptor
-  const uint32_t np = (n + 1u) >> 1;
-  const uint32_t K = np < nwaves ? np : nwaves;
+  // ---- the wave's static run: spans [sbase, sbase + m), m <= 64 (q or
+  // q + 1 of them: runs of pairs left a wave 25 % more than the mean on an
+  // SST file); lane j holds span sbase + j's descriptor.  The last
+  // `reserve` waves get no run: they take the long spans' tickets while the
+  // others stream their runs (a ticket is a few dependent memory round trips,
+  // ~5 us each under full load, too slow for the kernel's tail).
+  uint32_t reserve = nwaves / 32u;
+  if ((uint64_t)n + 64u * reserve > 64ull * nwaves) reserve = (64u * nwaves - n) / 64u;  // host: n <= 64 nwaves
+  const uint32_t K = n < nwaves - reserve ? n : nwaves - reserve;
+  // Ticket workers: the last waves without a run, at most 256 (every worker
+  // reads `word`, and reads of one address serialize in its L2 channel:
+  // ~2.5 ns each, 3072 of them cost ~8 us).
+  const uint32_t workers = nwaves - K < 256u ? nwaves - K : 256u;
+  const bool worker = wave >= nwaves - workers;
   uint32_t sbase = 0, m = 0;
   if (wave < K) {
-    const uint32_t q = np / K, r = np % K;
-    const uint32_t plo = wave * q + (wave < r ? wave : r);
-    const uint32_t phi = plo + q + (wave < r ? 1u : 0u);
-    sbase = 2u * plo;
-    m = (2u * phi < n ? 2u * phi : n) - sbase;
+    const uint32_t q = n / K, r = n % K;
+    sbase = wave * q + (wave < r ? wave : r);
+    m = q + (wave < r ? 1u : 0u);
   }
   uint32_t voff_lo = 0, voff_hi = 0, vlen = 0, vinit = 0;
   if (lane < m) {
@@ -215,7 +234,9 @@ __global__ __launch_bounds__(kDirectThreads) void crc32c_direct_kernel(SpanBatch
   // A group without static work, adopted tickets, whole spans or visible
   // tickets leaves before loading the tables.  (The OR over the group goes
   // through the table area: the tables take all of LDS.)
-  bool work = m != 0u || adopt_lo < adopt_hi;
+  // (the reserved waves -- the last ones, whose groups start last -- stay for
+  // pushes still to come)
+  bool work = m != 0u || adopt_lo < adopt_hi || worker;
   if (!work && lane == 0) {
     const uint64_t wd = __hip_atomic_load(d.word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     work = (uint32_t)(wd >> 32) > (uint32_t)wd;
@@ -302,12 +323,17 @@ __global__ __launch_bounds__(kDirectThreads) void crc32c_direct_kernel(SpanBatch
       for (uint32_t c = t.c; c < t.c1; c += 2u) {
         const bool two = c + 1u < t.c1;
         uint32_t w0[kRounds], w1[kRounds];
-        const uint32_t i0 = (c << 10) + lane - pad;  // may wrap: out of range, reads 0
+        const uint32_t i0 = (c << 10) + lane - pad;  // chunk 0: wraps below the body
 #pragma unroll
         for (int j = 0; j < kRounds; ++j) {
-          w0[j] = __builtin_amdgcn_raw_buffer_load_b32(rb, (int)((i0 + 64u * (uint32_t)j) * 4u), 0, 0);
-          w1[j] = two ? __builtin_amdgcn_raw_buffer_load_b32(rb, (int)((i0 + 1024u + 64u * (uint32_t)j) * 4u), 0, 0)
-                      : 0u;
+          // One opaque voffset per round: folded into the instruction's
+          // immediate offset, a wrapped (negative) voffset + imm is a sum past
+          // 2^32, which the range check reads as out of range -- zeros where
+          // chunk 0's body words are (the span kernel's note on chunk 0).
+          uint32_t o0 = (i0 + 64u * (uint32_t)j) * 4u, o1 = o0 + 4096u;
+          asm volatile("" : "+v"(o0), "+v"(o1));
+          w0[j] = __builtin_amdgcn_raw_buffer_load_b32(rb, (int)o0, 0, 0);
+          w1[j] = two ? __builtin_amdgcn_raw_buffer_load_b32(rb, (int)o1, 0, 0) : 0u;
         }
         if (c == 0u && t.z != 0u) inject(w0, pad, r0);
 #pragma unroll
@@ -394,30 +420,50 @@ __global__ __launch_bounds__(kDirectThreads) void crc32c_direct_kernel(SpanBatch
     // ---- early: this wave's orphans, its whole spans, up to two claims
     for (uint32_t tkt = adopt_lo; tkt < adopt_hi; ++tkt) run_ticket(tkt);
     for (uint64_t wm = whole; wm != 0u; wm &= wm - 1u) run_whole((uint32_t)__builtin_ctzll(wm));
-    {
-      uint64_t wd = 0;
-      if (lane == 0) wd = __hip_atomic_load(d.word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const uint32_t S = readlane((uint32_t)(wd >> 32), 0), C = readlane((uint32_t)wd, 0);
-      if (S > C) {
-        const uint32_t k = S - C >= 2u ? 2u : 1u;
+    // A worker waits up to ~5 us for the first push (bounded: nothing ever
+    // waits for another wave's progress), then claims tickets one at a time
+    // until none is left.  (All 2048 waves claiming at once after the table
+    // load serialized ~2048 atomics on one address, ~70 us.)
+    if (worker) {
+      if (d.dbg & 2u) {  // test hook: one blind claim (an orphan while nothing is pushed)
         uint32_t c = 0, sp = 0;
-        claim(k, c, sp);
-        const uint32_t got = sp > c ? (sp - c >= k ? k : sp - c) : 0u;
-        if (lane == 0 && got) atomicAdd(d.stats + 2, got);
-        for (uint32_t i = 0; i < got; ++i)
-          if (c + i < d.cap) run_ticket(c + i);
+        claim(1u, c, sp);
+        if (c < sp) {
+          if (lane == 0) atomicAdd(d.stats + 2, 1u);
+          if (c < d.cap) run_ticket(c);
+        }
+      }
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      for (;;) {
+        uint64_t wd = 0;
+        if (lane == 0) wd = __hip_atomic_load(d.word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t S = readlane((uint32_t)(wd >> 32), 0), C = readlane((uint32_t)wd, 0);
+        if (S > C) {
+          uint32_t c = 0, sp = 0;
+          claim(1u, c, sp);
+          if (c >= sp) break;  // an orphan: its pusher does it
+          if (lane == 0) atomicAdd(d.stats + 2, 1u);
+          if (c < d.cap) run_ticket(c);
+          continue;
+        }
+        if (__builtin_amdgcn_s_memrealtime() - t0 > 500u) break;  // 100 MHz: 5 us
+        __builtin_amdgcn_s_sleep(32);
       }
     }
 
-    // ---- the static run: one-chunk spans, stream st taking run positions
-    // st, st + 2, ... (long ones skipped).  Ring of two slots x two streams,
-    // inline-asm loads, counted waits -- crc32c_span_kernel's pair runs.
+    // ---- the static run: one-chunk spans, stream st (of three) taking run
+    // positions st, st + 3, ... (long ones skipped).  Ring of two slots x
+    // three streams (six tasks, 102 loads in flight; a wait leaves the other
+    // slot's 51 younger loads in flight, under vmcnt's 63), inline-asm
+    // loads, counted waits -- crc32c_span_kernel's ring with a third chain.
+    // With 12 waves per CU, an SST file's ~5.6 spans per wave are all
+    // requested at once.
     if (m != 0u) {
       const uint64_t inrun = m >= 64u ? ~0ull : (1ull << m) - 1ull;
       const uint64_t shortm = inrun & ~lm;
-      // next short span of stream st at or after position j: (slot, geometry)
+      // next short span of stream st at or after position j
       auto static_task = [&](uint32_t& j, uint32_t st) -> DTask {
-        const uint64_t par = st ? 0xAAAAAAAAAAAAAAAAull : 0x5555555555555555ull;
+        const uint64_t par = 0x9249249249249249ull << st;  // positions st mod 3
         const uint64_t from = j >= 64u ? 0ull : ~0ull << j;
         const uint64_t avail = shortm & par & from;
         if (avail == 0u) {
@@ -431,7 +477,7 @@ __global__ __launch_bounds__(kDirectThreads) void crc32c_direct_kernel(SpanBatch
         DTask t = geometry(base + off, readlane(vlen, p));
         t.b = sbase + p;
         t.f |= (kKindStatic << 14) | (p << 17);
-        j = p + 2u;
+        j = p + 3u;
         return t;
       };
       // 17 loads per task, always: 16 body dwords (the buffer range check
@@ -467,65 +513,77 @@ __global__ __launch_bounds__(kDirectThreads) void crc32c_direct_kernel(SpanBatch
         if (kVerify && lane >= 6u && lane < 10u) eoff = hwin ? lane - 6u : sat((uint64_t)len + (lane - 6u));
         e = buf_ubyte(re, eoff);
       };
-      auto fold = [&](const DTask& tx, uint32_t (&wx)[kRounds], uint32_t ex, const DTask& ty,
-                      uint32_t (&wy)[kRounds], uint32_t ey) {
-        // initial registers (init fed the head bytes) into body word 0
-        const uint32_t rx = feed_short(ss, lane, readlane(vinit, tx.slot()) ^ kConditioning, edge_head(ex, tx.h()), tx.h());
-        const uint32_t ry = feed_short(ss, lane, readlane(vinit, ty.slot()) ^ kConditioning, edge_head(ey, ty.h()), ty.h());
-        if (tx.z) inject(wx, tx.pad(), rx);
-        if (ty.z) inject(wy, ty.pad(), ry);
-        uint32_t ax = 0, ay = 0;
+      auto fold = [&](const DTask (&t)[3], uint32_t (&w)[3][kRounds], const uint32_t (&e)[3]) {
+        uint32_t r[3], acc[3] = {0u, 0u, 0u};
+#pragma unroll
+        for (int st = 0; st < 3; ++st) {
+          // initial register (init fed the head bytes) into body word 0
+          r[st] = feed_short(ss, lane, readlane(vinit, t[st].slot()) ^ kConditioning, edge_head(e[st], t[st].h()),
+                             t[st].h());
+          if (t[st].z) inject(w[st], t[st].pad(), r[st]);
+        }
 #pragma unroll
         for (int j = 0; j < kRounds; ++j) {
-          ax = step256(lds, tab, ax, wx[j]);
-          ay = step256(lds, tab, ay, wy[j]);
+#pragma unroll
+          for (int st = 0; st < 3; ++st) acc[st] = step256(lds, tab, acc[st], w[st][j]);
         }
-        const uint32_t vx = realign(lds, nibtab, ax), vy = realign(lds, nibtab, ay);
-        const uint32_t bx = wave_xor(vx), by = wave_xor(vy);
-        if (tx.valid()) finish(tx, tx.z ? bx : rx, edge_tail(ex, tx.t()), edge_stored(ex), true);
-        if (ty.valid()) finish(ty, ty.z ? by : ry, edge_tail(ey, ty.t()), edge_stored(ey), true);
+        uint32_t v[3];
+#pragma unroll
+        for (int st = 0; st < 3; ++st) v[st] = realign(lds, nibtab, acc[st]);
+#pragma unroll
+        for (int st = 0; st < 3; ++st) {
+          const uint32_t bv = wave_xor(v[st]);
+          if (t[st].valid()) finish(t[st], t[st].z ? bv : r[st], edge_tail(e[st], t[st].t()), edge_stored(e[st]), true);
+        }
       };
-      DTask tk[2][2];
-      uint32_t wb[2][2][kRounds];
-      uint32_t eb[2][2];
-      uint32_t j0 = 0, j1 = 1;
+      DTask tk[2][3];
+      uint32_t wb[2][3][kRounds];
+      uint32_t eb[2][3];
+      uint32_t jc[3] = {0u, 1u, 2u};
 #pragma unroll
       for (int sl = 0; sl < 2; ++sl) {
-        tk[sl][0] = static_task(j0, 0u);
-        tk[sl][1] = static_task(j1, 1u);
+#pragma unroll
+        for (int st = 0; st < 3; ++st) tk[sl][st] = static_task(jc[st], (uint32_t)st);
       }
-      if (tk[0][0].valid() || tk[0][1].valid()) {
+      if (tk[0][0].valid() || tk[0][1].valid() || tk[0][2].valid()) {
 #pragma unroll
         for (int sl = 0; sl < 2; ++sl) {
-          issue(tk[sl][0], wb[sl][0], eb[sl][0]);
-          issue(tk[sl][1], wb[sl][1], eb[sl][1]);
+#pragma unroll
+          for (int st = 0; st < 3; ++st) issue(tk[sl][st], wb[sl][st], eb[sl][st]);
         }
-        constexpr int kYounger = 2 * (kRounds + 1);  // the other slot's two tasks
+        constexpr int kYounger = 3 * (kRounds + 1);  // the other slot's three tasks
+        static_assert(kYounger <= 63, "vmcnt counts at most 63 loads");
         for (;;) {
 #pragma unroll
           for (int sl = 0; sl < 2; ++sl) {
-            wait_task<kYounger>(wb[sl][0], eb[sl][0]);
-            wait_task<kYounger>(wb[sl][1], eb[sl][1]);
-            fold(tk[sl][0], wb[sl][0], eb[sl][0], tk[sl][1], wb[sl][1], eb[sl][1]);
-            if (!tk[sl ^ 1][0].valid() && !tk[sl ^ 1][1].valid()) goto drained;
-            tk[sl][0] = static_task(j0, 0u);
-            tk[sl][1] = static_task(j1, 1u);
-            issue(tk[sl][0], wb[sl][0], eb[sl][0]);
-            issue(tk[sl][1], wb[sl][1], eb[sl][1]);
+#pragma unroll
+            for (int st = 0; st < 3; ++st) wait_task<kYounger>(wb[sl][st], eb[sl][st]);
+            fold(tk[sl], wb[sl], eb[sl]);
+            if (!tk[sl ^ 1][0].valid() && !tk[sl ^ 1][1].valid() && !tk[sl ^ 1][2].valid()) goto drained;
+#pragma unroll
+            for (int st = 0; st < 3; ++st) tk[sl][st] = static_task(jc[st], (uint32_t)st);
+#pragma unroll
+            for (int st = 0; st < 3; ++st) issue(tk[sl][st], wb[sl][st], eb[sl][st]);
           }
         }
       drained:
 #pragma unroll
         for (int sl = 0; sl < 2; ++sl) {
-          wait_task<0>(wb[sl][0], eb[sl][0]);
-          wait_task<0>(wb[sl][1], eb[sl][1]);
+#pragma unroll
+          for (int st = 0; st < 3; ++st) wait_task<0>(wb[sl][st], eb[sl][st]);
         }
       }
     }
 
-    // ---- late: claims, one ticket at a time, until none is left (a claim
-    // past the supply is an orphan: its pusher does it)
-    for (;;) {
+    // ---- late: a wave that pushed tickets claims, one at a time, until
+    // none is left -- its own included, whoever else did not take them, so
+    // every pushed ticket is claimed by someone (a claim past the supply is an
+    // orphan: its pusher does it).  Other static waves leave: 3072 reads of
+    // `word` at the end cost ~8 us of the kernel's tail.
+    while (lm != 0u && whole == 0u) {
+      uint64_t wd = 0;
+      if (lane == 0) wd = __hip_atomic_load(d.word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (readlane((uint32_t)(wd >> 32), 0) <= readlane((uint32_t)wd, 0)) break;
       uint32_t c = 0, sp = 0;
       claim(1u, c, sp);
       if (c >= sp) break;

@@ -115,21 +115,26 @@ __device__ __forceinline__ StrideLanes stride_lanes(uint32_t lane) {
   return t;
 }
 
-// Fill LDS with the image above.  Thread i reads table word i once (4 KiB per
-// group from L2) and writes its 32 copies -- 128 contiguous bytes -- as eight
-// 16-B stores; the per-lane nibble tables (32 KiB) are copied 16 B at a time.
-// (Reading every LDS word from global memory was 160 KiB of L2 reads per group,
-// one dependent load round per 1024 words.)
+// Fill LDS with the image above.  The image is 1024 segments of 128 B, one
+// per (table k, entry e): segment q = (k >> 1) << 9 | e << 1 | (k & 1) holds
+// the 32 copies of stride[k][e].  Lane x of a write writes 16 B (four copies)
+// of segment x / 8, so a wave writes 1 KiB of consecutive LDS: no bank
+// conflicts.  (One thread per table word writing its 128 B put every lane of
+// a wave 256 B apart -- all on the same four banks -- and took ~4 us per
+// group; one LDS word per thread, round 2's fill, needs 4x the instructions.)
+// The table words come from L1 (eight lanes read each).  The per-lane nibble
+// tables (32 KiB) are copied 16 B per lane, also consecutive.
 template <int kT>
 __device__ __forceinline__ void load_stride_image(uint32_t* lds, const uint32_t* tab, uint32_t tid) {
   typedef uint32_t v4 __attribute__((ext_vector_type(4)));
-  for (uint32_t i = tid; i < 1024u; i += kT) {
-    const uint32_t v = tab[i];
-    const uint32_t k = i >> 8, e = i & 255u;
-    v4* dst = reinterpret_cast<v4*>(lds + (((k >> 1) << 14) | (e << 6) | ((k & 1u) << 5)));
-    const v4 q = {v, v, v, v};
-#pragma unroll
-    for (int c = 0; c < 8; ++c) dst[c] = q;
+  v4* dst = reinterpret_cast<v4*>(lds);
+#pragma unroll 4
+  for (uint32_t x = tid; x < 8192u; x += kT) {
+    const uint32_t q = x >> 3;
+    const uint32_t k = ((q >> 9) << 1) | (q & 1u), e = (q >> 1) & 255u;
+    const uint32_t v = tab[k * 256u + e];
+    const v4 w = {v, v, v, v};
+    dst[x] = w;
   }
 }
 

@@ -156,11 +156,11 @@ int leveldb_sst_block_spans(const char* file, size_t file_size, uint64_t* off, u
 
   // Metaindex: "filter.<name>" -> filter block.  Its own trailer is part of
   // the batch, so a damaged metaindex shows up as a mismatch; it is only
-  // walked if it is stored uncompressed and parses.  A snappy metaindex with a
-  // good checksum hides the filter block's handle: unsupported, as above.
+  // walked if it is stored uncompressed and parses.  A snappy or unknown-type
+  // metaindex is not walked (no filter span) but still verified: the
+  // reference does not propagate metaindex errors either (Table::ReadMeta,
+  // table/table.cc:84-111, "Do not propagate errors"), Table::Open succeeds.
   const uint8_t* mb = f + meta.offset;
-  if (mb[meta.size] == kSnappyCompression && HostVerify(mb, meta.size))
-    return Unsupported("snappy-compressed metaindex block");
   if (mb[meta.size] == kNoCompression)
     ForEachEntry(mb, (size_t)meta.size, [&](const std::string& key, const uint8_t* v, size_t vn) {
       if (key.compare(0, 7, "filter.") == 0) {

@@ -98,12 +98,17 @@ class VerifyResult:
         return [b for b in self.blocks if b.status != OK]
 
 
-def verify_tables(images: Sequence[bytes], device=None, stream=None) -> VerifyResult:
+def verify_tables(images: Sequence[bytes], device=None, stream=None, check_bounds: bool = True) -> VerifyResult:
     """Verify every block of every SST image with one device batch.
 
     The images are packed back to back into one device buffer (as a compaction
     would stage its input files), spans are collected per image, and one
-    leveldb_crc32c_batch with a mismatch vector covers them all."""
+    leveldb_crc32c_batch with a mismatch vector covers them all.
+
+    check_bounds: the spans (each with its 4-byte trailer) are checked against
+    their image on the host, where they already are -- no device reduction or
+    extra sync; the parser (leveldb_sst_block_spans) already rejects handles
+    past the file, so False only skips this second look."""
     import numpy as np
     import torch
 
@@ -121,6 +126,8 @@ def verify_tables(images: Sequence[bytes], device=None, stream=None) -> VerifyRe
         offs.append(o + np.uint64(base))
         lens.append(ln)
         kinds.append(k)
+        if check_bounds and len(o) and int((o + ln.astype(np.uint64) + np.uint64(4)).max()) > len(img):
+            raise ValueError(f"image {t}: a block span reaches past the file ({len(img)} bytes)")
         tabs.append(np.full(len(o), t, dtype=np.int64))
         base += (len(img) + 15) & ~15
     blob = np.zeros(base, dtype=np.uint8)
@@ -138,7 +145,7 @@ def verify_tables(images: Sequence[bytes], device=None, stream=None) -> VerifyRe
             d_buf = torch.from_numpy(blob).to(dev, non_blocking=True)
             d_off = torch.from_numpy(off.astype(np.int64)).to(dev)
             d_len = torch.from_numpy(ln.view(np.int32)).to(dev)
-            _, mm = crc32c.batch(d_buf, d_off, d_len, verify=True)
+            _, mm = crc32c.batch(d_buf, d_off, d_len, verify=True, check_bounds=False)  # checked above
             bad = mm.cpu().numpy()
         for i in range(len(off)):
             t = int(tab[i])
@@ -147,15 +154,17 @@ def verify_tables(images: Sequence[bytes], device=None, stream=None) -> VerifyRe
     return VerifyResult(blocks, errors)
 
 
-def seal_blocks(buf, off, size, *, stream=None):
+def seal_blocks(buf, off, size, *, stream=None, check_bounds: bool = True):
     """Write `type || LE32(Mask(crc32c(contents || type)))` trailers in place.
 
     buf: device uint8 tensor holding blocks at off[i] (int64) with size[i]
     (int32) content bytes, the type byte already at off[i]+size[i]; the 4
-    bytes after it are overwritten.  Returns the masked CRCs (int32)."""
+    bytes after it are overwritten.  Returns the masked CRCs (int32).
+    check_bounds as for crc32c.batch (True blocks the host on a device
+    reduction; pass False for descriptors already checked)."""
     import torch
 
     with torch.cuda.stream(stream) if stream is not None else nullcontext():
         lens = size + 1
-        out, _ = crc32c.batch(buf, off, lens, mask=True, trailer=True)
+        out, _ = crc32c.batch(buf, off, lens, mask=True, trailer=True, check_bounds=check_bounds)
     return out

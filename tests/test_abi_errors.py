@@ -127,3 +127,46 @@ def test_python_host_batch_bounds(native):
         crc32c.batch_host(data, off, np.array([10], dtype=np.uint32))
     with pytest.raises(ValueError, match="same length"):
         crc32c.batch_host(data, off, np.array([10, 10], dtype=np.uint32), init=np.array([1], dtype=np.uint32))
+
+
+def test_python_host_batch_offsets_do_not_wrap(native):
+    """A negative offset (-1 would wrap to 2^64 - 1) and an offset past the
+    buffer whose end wraps back inside it are rejected, not passed on."""
+    from prismdb_amd import crc32c
+
+    data = np.zeros(8192, dtype=np.uint8)
+    with pytest.raises(ValueError, match="negative"):
+        crc32c.batch_host(data, np.array([-1, 0], dtype=np.int64), np.array([1, 10], dtype=np.uint32))
+    wrap = np.array([0, 2**64 - 16], dtype=np.uint64)  # + 32 wraps to 16
+    with pytest.raises(ValueError, match="outside"):
+        crc32c.batch_host(data, wrap, np.array([10, 32], dtype=np.uint32))
+
+
+def _multi(native, ndev, devices, base, off, ln, n, out, mm=None, flags=0, init=None):
+    P = ctypes.c_void_p * max(ndev, 1)
+    return native.leveldb_crc32c_batch_multi(
+        ndev, (ctypes.c_int * len(devices))(*devices) if devices is not None else None,
+        P(*base) if base is not None else None, P(*off) if off is not None else None,
+        P(*ln) if ln is not None else None, P(*init) if init is not None else None,
+        (ctypes.c_size_t * len(n))(*n) if n is not None else None, out, mm, flags, None)
+
+
+def test_multi_argument_checks(native, bufs):
+    """leveldb_crc32c_batch_multi checks its arguments before any device or
+    RCCL call: device count, NULL arrays, a device listed twice, a
+    partition's NULL descriptors, results wanted somewhere, flags."""
+    data, off, ln, out, mm = bufs
+    b, o, l, po = data.ctypes.data, off.ctypes.data, ln.ctypes.data, out.ctypes.data
+    assert _multi(native, 0, [0], [b], [o], [l], [4], po) == EINVAL and "ndev" in _err(native)
+    assert _multi(native, 65, [0], [b], [o], [l], [4], po) == EINVAL and "ndev" in _err(native)
+    assert _multi(native, 1, None, [b], [o], [l], [4], po) == EINVAL and "non-NULL" in _err(native)
+    assert _multi(native, 1, [0], [b], [o], [l], None, po) == EINVAL and "non-NULL" in _err(native)
+    assert _multi(native, 2, [0, 0], [b, b], [o, o], [l, l], [4, 4], po) == EINVAL
+    assert "twice" in _err(native)
+    assert _multi(native, 1, [-1], [b], [o], [l], [4], po) == EINVAL and "negative" in _err(native)
+    assert _multi(native, 2, [0, 1], [b, None], [o, o], [l, l], [4, 4], po) == EINVAL
+    assert "NULL" in _err(native)
+    assert _multi(native, 1, [0], [b], [o], [l], [4], None) == EINVAL and "out0 or mismatch0" in _err(native)
+    assert _multi(native, 1, [0], [b], [o], [l], [4], po, flags=0x10) == EINVAL and "flag" in _err(native)
+    assert _multi(native, 1, [0], [b], [o], [l], [4], po, mm.ctypes.data, WRITE_TRAILER) == EINVAL
+    assert "exclusive" in _err(native)

@@ -6,6 +6,7 @@ machinery: tickets of long spans claimed by any wave, the combine, the
 whole-span fallback when the ticket workspace is full, orphaned claims
 adopted by a late pusher.  Bit-exact against the oracle."""
 import ctypes
+import threading
 
 import numpy as np
 import pytest
@@ -47,8 +48,8 @@ def _sst_file(oracle, seed, files=1):
     its masked crc stored after it (a sealed file).  Returns host bytes,
     offsets, lengths and the masked crcs."""
     fbytes = ND * STRIDE + INDEX + 4
-    off1 = np.concatenate([np.arange(ND, dtype=np.uint64) * STRIDE, [ND * STRIDE]])
-    len1 = np.concatenate([np.full(ND, DATA, dtype=np.uint32), [INDEX]])
+    off1 = np.concatenate([np.arange(ND, dtype=np.uint64) * STRIDE, np.array([ND * STRIDE], dtype=np.uint64)])
+    len1 = np.concatenate([np.full(ND, DATA, dtype=np.uint32), np.array([INDEX], dtype=np.uint32)])
     host = oracle.synth(files * fbytes + 64, seed)
     off = (np.arange(files, dtype=np.uint64)[:, None] * fbytes + off1[None, :]).reshape(-1) + 8
     lens = np.tile(len1, files)
@@ -95,7 +96,7 @@ def test_sst_file_calls_back_to_back(dev, oracle, native):
 def test_sst_files_verify_damaged(dev, oracle, native, files):
     """Verify one and seven files per call (7 x 16 812 spans: the one-launch
     limit is 2^17) with damaged data blocks, a damaged index block (its
-    tickets) and a damaged trailer; a non-zero init on every span."""
+    tickets) and a damaged trailer; then a non-zero init on every span."""
     import torch
     from prismdb_amd import crc32c
 
@@ -105,16 +106,20 @@ def test_sst_files_verify_damaged(dev, oracle, native, files):
     for v in victims[:3]:
         host[int(off[v]) + int(lens[v]) // 3] ^= 0x11
     host[int(off[victims[3]]) + int(lens[victims[3]]) + 1] ^= 0x80  # trailer byte
-    init = (np.arange(n, dtype=np.uint64) * 0x9E3779B1 % (1 << 32)).astype(np.uint32)
-    want, wmm = oracle.batch(host, off, lens, init, mask=True, verify=True)
+    want, wmm = oracle.batch(host, off, lens, verify=True)
     buf = torch.from_numpy(host).to(dev)
-    out, mm = crc32c.batch(buf, torch.from_numpy(off.astype(np.int64)).to(dev),
-                           torch.from_numpy(lens.view(np.int32)).to(dev),
-                           torch.from_numpy(init.view(np.int32)).to(dev), mask=True, verify=True)
+    d_off = torch.from_numpy(off.astype(np.int64)).to(dev)
+    d_len = torch.from_numpy(lens.view(np.int32)).to(dev)
+    out, mm = crc32c.batch(buf, d_off, d_len, verify=True)
     assert _last_split_rc(native) == -2
     np.testing.assert_array_equal(_u32(out), want)
     np.testing.assert_array_equal(mm.cpu().numpy(), wmm)
     assert sorted(np.flatnonzero(mm.cpu().numpy()).tolist()) == sorted(set(victims))
+    # a non-zero init on every span (Extend), masked
+    init = (np.arange(n, dtype=np.uint64) * 0x9E3779B1 % (1 << 32)).astype(np.uint32)
+    want2, _ = oracle.batch(host, off, lens, init, mask=True)
+    out2, _ = crc32c.batch(buf, d_off, d_len, torch.from_numpy(init.view(np.int32)).to(dev), mask=True)
+    np.testing.assert_array_equal(_u32(out2), want2)
 
 
 def test_tickets_claimed_and_combined(dev, oracle, native):
@@ -193,11 +198,14 @@ def test_ticket_workspace_full_whole_spans(dev, oracle, native):
     np.testing.assert_array_equal(_u32(out2), want)
 
 
-def test_orphaned_claims_adopted(dev, oracle, native):
-    """Pushes delayed ~100 us (test hook): the other waves finish their runs
-    and claim past the supply first; the late pusher finds its tickets claimed
-    by waves that left (orphans) and folds them itself.  An SST file with
-    sealed trailers, verify."""
+@pytest.mark.parametrize("dbg", [1, 3])
+def test_late_push_and_orphans(dev, oracle, native, dbg):
+    """Pushes delayed ~100 us (test hook bit 0): the ticket workers have
+    stopped waiting, so the late pusher claims its own tickets after its run
+    (stats[3]).  With bit 1 every worker first makes one blind claim: those
+    past the supply are orphans, which the pusher finds claimed and folds
+    itself (stats[0]).  An SST file with sealed trailers, verify; every
+    ticket accounted for exactly once."""
     import torch
     from prismdb_amd import crc32c
 
@@ -207,7 +215,7 @@ def test_orphaned_claims_adopted(dev, oracle, native):
     d_len = torch.from_numpy(lens.view(np.int32)).to(dev)
     crc32c.batch(buf, d_off[:1], d_len[:1])
     before = _stats(native)
-    prev = native.prismdb_crc32c_direct_debug(1)
+    prev = native.prismdb_crc32c_direct_debug(dbg)
     try:
         out, mm = crc32c.batch(buf, d_off, d_len, verify=True, check_bounds=False)
         got, gmm = _u32(out), mm.cpu().numpy()
@@ -216,7 +224,17 @@ def test_orphaned_claims_adopted(dev, oracle, native):
         native.prismdb_crc32c_direct_debug(prev)
     np.testing.assert_array_equal(got, raw)
     assert (gmm == 0).all()
-    assert (after - before)[0] > 0  # tickets adopted
+    d = after - before
+    nch = (int(lens[-1]) + 4095) // 4096  # the index block (8-B aligned, offset multiple of 4)
+    per = (nch + 63) // 64
+    lg = 0 if per <= 1 else 1 if per <= 2 else 2 if per <= 4 else 3
+    T = (nch + (1 << lg) - 1) >> lg
+    assert d[0] + d[2] + d[3] == T, (d, T)
+    assert d[1] == 0
+    if dbg == 3:
+        assert d[0] > 0  # orphans adopted
+    else:
+        assert d[3] > 0  # the pusher's own late claims
 
 
 def test_direct_limit(dev, oracle, native):
@@ -274,3 +292,55 @@ def test_direct_concurrent_threads(dev, oracle):
     for x in th:
         x.join(120)
     assert not errors, errors
+
+
+def test_thread_churn_device_memory_flat(dev, oracle, native):
+    """64 short-lived caller threads (8 at a time), each with its own stream,
+    one one-launch call and one planner call (two workspaces' worth of device
+    memory, > 50 MiB per thread): when a thread exits its workspaces go back
+    (stream-ordered frees behind the thread's last batch, pool trimmed), so
+    free device memory afterwards is where it was -- and the results are
+    right throughout."""
+    import torch
+    from prismdb_amd import crc32c
+
+    host, off, lens, raw, masked = _sst_file(oracle, 0x5EED00DA)
+    buf = torch.from_numpy(host).to(dev)
+    d_off = torch.from_numpy(off.astype(np.int64)).to(dev)
+    d_len = torch.from_numpy(lens.view(np.int32)).to(dev)
+    errors = []
+
+    def run(t):
+        try:
+            s = torch.cuda.Stream()
+            with torch.cuda.stream(s):
+                out = torch.empty((2, len(off)), dtype=torch.int32, device=dev)
+                crc32c.batch(buf, d_off, d_len, out=out[0], check_bounds=False, stream=s)  # one launch
+                prev = native.prismdb_crc32c_direct_max(0)  # (global hook: only this test's threads call)
+                crc32c.batch(buf, d_off, d_len, out=out[1], check_bounds=False, stream=s)  # planner
+                native.prismdb_crc32c_direct_max(prev)
+                s.synchronize()
+                if not (out.cpu().numpy().view(np.uint32) == raw[None, :]).all():
+                    errors.append(t)
+        except Exception as e:  # noqa: BLE001 - reported below
+            errors.append((t, repr(e)))
+
+    def wave(first):
+        th = [threading.Thread(target=run, args=(first + t,)) for t in range(8)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join(120)
+
+    wave(0)  # torch's own per-thread state and the tensors above exist from here on
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    free0, _ = torch.cuda.mem_get_info(dev)
+    for w in range(1, 8):
+        wave(8 * w)
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    free1, _ = torch.cuda.mem_get_info(dev)
+    assert not errors, errors
+    # 56 leaked thread workspaces would be > 2.8 GiB
+    assert free0 - free1 < 256 << 20, (free0 - free1) / 2**20

@@ -1,0 +1,122 @@
+"""leveldb_crc32c_batch_multi: partitions on several devices of one process,
+results gathered over RCCL to the first device (include/prismdb_crc32c.h;
+PrismDB's per-partition background threads, db/db_impl.h:359).  On the
+1-GPU lease this runs at ndev = 1 (the clique, its streams, the scratch and
+the caller-stream handoff, with the gather a no-op); with more visible
+devices also across all of them.  Bit-exact against the oracle."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _u32(t):
+    return t.cpu().numpy().view(np.uint32)
+
+
+def _partition(oracle, seed, nblocks, long_every=0):
+    """An SST-shaped partition: 3988-B data spans at stride 3992 with every
+    `long_every`-th span a long (index-like) one, each followed by its
+    4-byte trailer."""
+    rng = np.random.default_rng(seed)
+    lens = np.full(nblocks, 3988, dtype=np.uint32)
+    if long_every:
+        lens[::long_every] = rng.integers(5000, 300_000, size=len(lens[::long_every]))
+    off = np.cumsum(np.concatenate([[8], (lens.astype(np.uint64) + 4)[:-1]])).astype(np.uint64)
+    host = oracle.synth(int(off[-1]) + int(lens[-1]) + 64, seed)
+    return host, off, lens
+
+
+def _to(dev, host, off, lens):
+    import torch
+
+    return (torch.from_numpy(host).to(dev), torch.from_numpy(off.astype(np.int64)).to(dev),
+            torch.from_numpy(lens.view(np.int32)).to(dev))
+
+
+@pytest.fixture(scope="module")
+def devices(native):
+    import torch
+
+    assert torch.cuda.is_available(), "gpu tests need a HIP device"
+    return list(range(torch.cuda.device_count()))
+
+
+@pytest.mark.parametrize("long_every", [0, 97])
+def test_multi_one_device_seal_then_verify(devices, oracle, long_every):
+    """ndev = 1: seal (MASK | WRITE_TRAILER) one partition, then verify it;
+    then damage three blocks and verify again."""
+    import torch
+    from prismdb_amd import crc32c
+
+    host, off, lens = _partition(oracle, 0x5EED0301 + long_every, 5000, long_every)
+    want, _ = oracle.batch(host, off, lens, mask=True)
+    dev = torch.device("cuda", devices[0])
+    buf, d_off, d_len = _to(dev, host, off, lens)
+    out, _ = crc32c.batch_multi([(buf, d_off, d_len)], mask=True, trailer=True)
+    np.testing.assert_array_equal(_u32(out), want)
+    sealed = buf.cpu().numpy()
+    tr = (off + lens.astype(np.uint64)).astype(np.int64)
+    np.testing.assert_array_equal(
+        sealed[tr[:, None] + np.arange(4)[None, :]].copy().view("<u4").reshape(-1), want)
+    raw, _ = oracle.batch(host, off, lens)
+    out, mm = crc32c.batch_multi([(buf, d_off, d_len)], verify=True)
+    np.testing.assert_array_equal(_u32(out), raw)
+    assert not mm.cpu().numpy().any()
+    bad = [0, 1234, 4999]
+    for i in bad:
+        buf[int(off[i]) + 7] ^= 0x40
+    out, mm = crc32c.batch_multi([(buf, d_off, d_len)], verify=True)
+    assert sorted(np.nonzero(mm.cpu().numpy())[0].tolist()) == bad
+
+
+def test_multi_one_device_streams_and_init(devices, oracle):
+    """ndev = 1 on a side stream with per-span initial registers: the call
+    orders after work already on the stream (the buffer is filled there) and
+    the stream waits for the results; repeated calls grow nothing."""
+    import torch
+    from prismdb_amd import crc32c
+
+    host, off, lens = _partition(oracle, 0x5EED0303, 3000, 50)
+    init = np.random.default_rng(3).integers(0, 2**32, size=len(off), dtype=np.uint64).astype(np.uint32)
+    want, _ = oracle.batch(host, off, lens, init, mask=True)
+    dev = torch.device("cuda", devices[0])
+    s = torch.cuda.Stream(dev)
+    with torch.cuda.stream(s):
+        buf = torch.empty(len(host), dtype=torch.uint8, device=dev)
+        buf.copy_(torch.from_numpy(host).pin_memory(), non_blocking=True)
+        d_off = torch.from_numpy(off.astype(np.int64)).to(dev)
+        d_len = torch.from_numpy(lens.view(np.int32)).to(dev)
+        d_init = torch.from_numpy(init.view(np.int32)).to(dev)
+    for _ in range(3):
+        out, _ = crc32c.batch_multi([(buf, d_off, d_len, d_init)], mask=True, streams=[s], check_bounds=False)
+        with torch.cuda.stream(s):
+            got = out.clone()
+        s.synchronize()
+        np.testing.assert_array_equal(_u32(got), want)
+
+
+def test_multi_all_devices(devices, oracle):
+    """Every visible device one partition (different sizes, one empty when
+    there are three or more); results gathered to the first, partition after
+    partition."""
+    import torch
+    from prismdb_amd import crc32c
+
+    if len(devices) < 2:
+        pytest.skip("one visible device: ndev = 1 is covered above")
+    parts, want = [], []
+    for k, d in enumerate(devices):
+        nb = 0 if (k == 2) else 1000 + 777 * k
+        if nb == 0:
+            dev = torch.device("cuda", d)
+            parts.append((torch.zeros(64, dtype=torch.uint8, device=dev), torch.zeros(0, dtype=torch.int64, device=dev),
+                          torch.zeros(0, dtype=torch.int32, device=dev)))
+            continue
+        host, off, lens = _partition(oracle, 0x5EED0310 + k, nb, 40)
+        w, _ = oracle.batch(host, off, lens, mask=True)
+        want.append(w)
+        parts.append(_to(torch.device("cuda", d), host, off, lens))
+    out, _ = crc32c.batch_multi(parts, mask=True)
+    assert out.device.index == devices[0]
+    np.testing.assert_array_equal(_u32(out), np.concatenate(want))

@@ -109,18 +109,38 @@ def _retype(f: bytearray, blk: dict, typ: int, oracle) -> None:
     f[o + n + 1:o + n + 5] = crc.to_bytes(4, "little")
 
 
-@pytest.mark.parametrize("kind", ["index", "metaindex"])
-def test_block_spans_snappy_index_unsupported(native, golden, oracle, kind):
-    """A table built with kSnappyCompression may store its index/metaindex
-    compressed (table/table_builder.cc:159): reported as NotSupported, never
-    parsed as raw entries."""
+def test_block_spans_snappy_index_unsupported(native, golden, oracle):
+    """A table built with kSnappyCompression may store its index compressed
+    (table/table_builder.cc:159): reported as NotSupported, never parsed as
+    raw entries."""
     from prismdb_amd import sst
 
     f = bytearray(golden["sst_bytes"])
-    blk = [b for b in golden["sst"]["blocks"] if b["kind"] == kind][0]
+    blk = [b for b in golden["sst"]["blocks"] if b["kind"] == "index"][0]
     _retype(f, blk, 1, oracle)
-    with pytest.raises(sst.SstUnsupported, match=f"Not implemented: snappy-compressed {kind} block"):
+    with pytest.raises(sst.SstUnsupported, match="Not implemented: snappy-compressed index block"):
         sst.block_spans(bytes(f))
+
+
+@pytest.mark.parametrize("typ", [1, 9])
+def test_block_spans_snappy_or_unknown_metaindex_skipped(native, golden, oracle, typ):
+    """A well-sealed snappy (1) or unknown-type (9) metaindex does not fail the
+    table -- Table::ReadMeta does not propagate metaindex errors
+    (table/table.cc:84-111) -- it is not walked, so no filter span, but it is
+    still listed (and its checksum verified by the batch)."""
+    from prismdb_amd import sst
+
+    f = bytearray(golden["sst_bytes"])
+    blk = [b for b in golden["sst"]["blocks"] if b["kind"] == "metaindex"][0]
+    _retype(f, blk, typ, oracle)
+    off, ln, kind = sst.block_spans(bytes(f))
+    names = [sst.KIND_NAMES[int(k)] for k in kind]
+    assert names.count("metaindex") == 1 and names.count("filter") == 0
+    assert names.count("data") == sum(1 for b in golden["sst"]["blocks"] if b["kind"] == "data")
+    i = names.index("metaindex")
+    o, n = int(off[i]), int(ln[i])
+    assert o == blk["offset"] and n == blk["size"] + 1
+    assert oracle.mask(oracle.value(bytes(f[o:o + n]))) == int.from_bytes(f[o + n:o + n + 4], "little")
 
 
 def test_block_spans_bad_index_type(native, golden, oracle):

@@ -205,8 +205,12 @@ def main():
     cin = [None] * len(bl)
 
     def is_threadable(n):
+        # short blocks without vector-memory ops or waits: hipcc's exit funnels
+        # (a vcc branch on a constant SGPR pair) and the one- or two-
+        # instruction blocks that lead into them (copies, then fall-through),
+        # so a constant set on one path survives to the branch that tests it
         a, b = bl[n]
-        if b - a > 8 or insts[b - 1][1].split()[0] not in ("s_cbranch_vccz", "s_cbranch_vccnz"):
+        if b - a > 8:
             return False
         return not any(insts[k][1].split()[0].startswith(VMEM) or insts[k][1].startswith("s_waitcnt")
                        for k in range(a, b))

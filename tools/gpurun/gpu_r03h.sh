@@ -1,0 +1,14 @@
+#!/bin/bash
+# one-launch path + batch_multi (ndev = 1) + thread churn: new tests first, full GPU suite, bench with the config-5 leg, kernel trace of the per-call tool
+set -o pipefail
+R=$GRAFT_REPO_ROOT; O=$R/gpurun_out; mkdir -p $O
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/r03h_smoke.log 2>&1 || { tail -20 $O/r03h_smoke.log; exit 1; }
+tail -1 $O/r03h_smoke.log
+timeout -k 10 300 python -u -m pytest tests/test_gpu_direct.py tests/test_gpu_multi.py -x -v --timeout 120 --timeout-method thread -m gpu > $O/r03h_new.log 2>&1 || { echo NEW_FAIL; tail -60 $O/r03h_new.log; exit 1; }
+tail -3 $O/r03h_new.log
+timeout -k 10 800 python -u -m pytest tests -x -q --timeout 300 --timeout-method thread -m gpu > $O/r03h_tests.log 2>&1 || { echo TESTS_FAIL; tail -40 $O/r03h_tests.log; exit 1; }
+tail -2 $O/r03h_tests.log
+timeout -k 10 400 python -u bench.py --steps 5 --warmup 2 > $O/r03h_bench.json 2> $O/r03h_bench.err || { tail -20 $O/r03h_bench.err; exit 1; }
+cat $O/r03h_bench.json
+export TMPDIR=/tmp
+cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/r03h_kt -o run --output-format csv -- python3 $R/tools/percall.py > $O/r03h_percall_under_rocprof.json 2> $O/r03h_kt.log
