@@ -51,16 +51,19 @@ def _run(cmd: list[str]) -> None:
 
 
 def build(force: bool = False, asm: bool = False, verbose: bool = False, defines: dict | None = None,
-          lib_path: str | None = None) -> str:
-    """Build the library.  `defines`/`lib_path` build a tuning variant
-    (e.g. {"PRISMDB_RING": 3}) to a separate file; the product is the default."""
+          lib_path: str | None = None, src_dir: str | None = None, obj_dir: str | None = None) -> str:
+    """Build the library.  The product is the default; tools/variants.py
+    builds measurement variants from a patched copy of the sources
+    (`src_dir`, `obj_dir`, `lib_path`), never from knobs in the product
+    source."""
     lib_out = lib_path or LIB
-    objdir = OBJDIR if not defines else os.path.join(ROOT, "build", "obj_" + "_".join(
-        f"{k}{v}" for k, v in sorted(defines.items())))
+    csrc = src_dir or CSRC
+    objdir = obj_dir or (OBJDIR if not defines else os.path.join(ROOT, "build", "obj_" + "_".join(
+        f"{k}{v}" for k, v in sorted(defines.items()))))
     os.makedirs(os.path.dirname(lib_out), exist_ok=True)
     os.makedirs(objdir, exist_ok=True)
     hipcc = _hipcc()
-    headers = [os.path.join(CSRC, h) for h in HEADERS] + [
+    headers = [os.path.join(csrc, h) for h in HEADERS] + [
         os.path.join(ROOT, "include", "prismdb_crc32c.h"),
         os.path.join(ROOT, "include", "prismdb_synth.h"),
         os.path.join(ROOT, "include", "prismdb_sst.h"),
@@ -72,7 +75,7 @@ def build(force: bool = False, asm: bool = False, verbose: bool = False, defines
     jobs = []
     objs = []
     for src in HIP_SOURCES + CXX_SOURCES:
-        s = os.path.join(CSRC, src)
+        s = os.path.join(csrc, src)
         o = os.path.join(objdir, src + ".o")
         objs.append(o)
         if force or _stale(o, [s] + headers):
@@ -86,7 +89,7 @@ def build(force: bool = False, asm: bool = False, verbose: bool = False, defines
             if verbose:
                 print(" ".join(cmd))
         list(ex.map(_run, jobs))
-    exports = os.path.join(CSRC, "exports.map")
+    exports = os.path.join(csrc, "exports.map")
     if force or jobs or _stale(lib_out, objs + [exports]):
         _run([hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", f"-Wl,--version-script={exports}",
               "-o", lib_out, *objs, "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"])
@@ -95,7 +98,7 @@ def build(force: bool = False, asm: bool = False, verbose: bool = False, defines
         os.makedirs(asmdir, exist_ok=True)
         for src in HIP_SOURCES:
             _run([hipcc, "-x", "hip", f"--offload-arch={ARCH}", *common, "--cuda-device-only", "-S",
-                  os.path.join(CSRC, src), "-o", os.path.join(asmdir, src + ".s")])
+                  os.path.join(csrc, src), "-o", os.path.join(asmdir, src + ".s")])
     return lib_out
 
 

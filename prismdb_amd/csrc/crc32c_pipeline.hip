@@ -13,16 +13,18 @@
 // stream has released it.  A pageable source is first staged into the slot's
 // pinned buffer by several host threads (one memcpy thread reaches about half
 // the link rate).  The call is synchronous (like ReadBlock) and thread-safe:
-// every calling thread gets its own ring per device.
+// a call leases a ring (its streams and slots) from a per-device pool for its
+// duration, so memory follows the number of CONCURRENT calls, not the number
+// of threads that ever called; at most kKeepIdle rings per device stay
+// allocated between calls (each ~256 MiB pinned + ~256 MiB device).
 #include <hip/hip_runtime.h>
-#include <sys/syscall.h>
-#include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <cstring>
-#include <map>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -40,11 +42,13 @@ constexpr size_t kMaxSpan = 64ull << 20;     // one 64 MiB SST (include/leveldb/
 constexpr size_t kSlotBytes = kMaxSpan + 8;  // a chunk holds one span of up to kMaxSpan
 constexpr size_t kChunkSpans = 1u << 16;     // descriptors per chunk
 constexpr int kDepth = 4;
+constexpr size_t kKeepIdle = 2;  // idle rings kept per device
+constexpr int kMaxDevices = 64;
 
 // Test hook (not in the public header, like prismdb_crc32c_force_generic):
 // the k-th chunk of every later call fails as a device error would, after the
 // earlier chunks have been enqueued.  0 = off.
-int g_fail_after_chunks = 0;
+std::atomic<int> g_fail_after_chunks{0};
 
 int PipeFail(int code, const std::string& msg) {
   prismdb::SetLastError(msg);
@@ -67,22 +71,26 @@ struct Slot {
 };
 
 struct Ring {
+  int device = 0;
   hipStream_t copy = nullptr, compute = nullptr;
   Slot slot[kDepth];
+  // Called with `device` current.  The ring's own streams are drained first;
+  // its device blocks go back stream-ordered (no device-wide hipFree).
   ~Ring() {
-    if (copy) hipStreamSynchronize(copy);
-    if (compute) hipStreamSynchronize(compute);
+    if (copy) (void)hipStreamSynchronize(copy);
+    if (compute) (void)hipStreamSynchronize(compute);
     for (Slot& s : slot) {
-      hipHostFree(s.h_stage);
-      hipHostFree(s.h_desc);
-      hipHostFree(s.h_out);
-      hipFree(s.d_data);
-      hipFree(s.d_desc);
-      if (s.copied) hipEventDestroy(s.copied);
-      if (s.done) hipEventDestroy(s.done);
+      (void)hipHostFree(s.h_stage);
+      (void)hipHostFree(s.h_desc);
+      (void)hipHostFree(s.h_out);
+      if (s.d_data) (void)hipFreeAsync(s.d_data, compute);
+      if (s.d_desc) (void)hipFreeAsync(s.d_desc, compute);
+      if (s.copied) (void)hipEventDestroy(s.copied);
+      if (s.done) (void)hipEventDestroy(s.done);
     }
-    if (copy) hipStreamDestroy(copy);
-    if (compute) hipStreamDestroy(compute);
+    if (compute) (void)hipStreamSynchronize(compute);
+    if (copy) (void)hipStreamDestroy(copy);
+    if (compute) (void)hipStreamDestroy(compute);
   }
 };
 
@@ -95,45 +103,73 @@ int MakeRing(Ring& r) {
     if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(&s.h_stage), kSlotBytes);
     if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(&s.h_desc), kChunkSpans * 16);
     if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(&s.h_out), kChunkSpans * (4 + 1));
-    if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&s.d_data), kSlotBytes);
-    if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&s.d_desc), kChunkSpans * (16 + 4 + 1));
+    if (e == hipSuccess) e = hipMallocAsync(reinterpret_cast<void**>(&s.d_data), kSlotBytes, r.compute);
+    if (e == hipSuccess) e = hipMallocAsync(reinterpret_cast<void**>(&s.d_desc), kChunkSpans * (16 + 4 + 1), r.compute);
     if (e != hipSuccess) break;
     s.h_mm = reinterpret_cast<uint8_t*>(s.h_out + kChunkSpans);
     s.d_out = reinterpret_cast<uint32_t*>(s.d_desc + kChunkSpans * 16);
     s.d_mm = reinterpret_cast<uint8_t*>(s.d_out + kChunkSpans);
   }
+  if (e == hipSuccess) e = hipStreamSynchronize(r.compute);
   if (e != hipSuccess) return PipeFail(PRISMDB_CRC32C_EDEVICE, std::string("pipeline setup: ") + hipGetErrorString(e));
   return 0;
 }
 
-// A worker thread's rings are released when it exits.  The main thread's are
-// left to the OS: its thread-local destructors run inside exit(), where the
-// HIP runtime (or a profiler wrapped around it) may already be tearing down.
-struct RingMap {
-  std::map<int, std::unique_ptr<Ring>> rings;
-  ~RingMap() {
-    if (syscall(SYS_gettid) == getpid())
-      for (auto& kv : rings) (void)kv.second.release();
+// Idle rings per device.  The pool itself is never destroyed: at exit() the
+// HIP runtime (or a profiler wrapped around it) may already be tearing down,
+// so the rings still in it are left to the OS.
+struct RingPool {
+  std::mutex mu;
+  std::vector<Ring*> idle[kMaxDevices];
+};
+RingPool& Pool() {
+  static RingPool* pool = new RingPool;
+  return *pool;
+}
+
+// A ring for the duration of one call (current device).
+struct RingLease {
+  Ring* ring = nullptr;
+  int Acquire() {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return PipeFail(PRISMDB_CRC32C_EDEVICE, std::string("hipGetDevice: ") + hipGetErrorString(e));
+    if (dev < 0 || dev >= kMaxDevices) return PipeFail(PRISMDB_CRC32C_EINVAL, "device ordinal out of range");
+    {
+      std::lock_guard<std::mutex> lk(Pool().mu);
+      std::vector<Ring*>& idle = Pool().idle[dev];
+      if (!idle.empty()) {
+        ring = idle.back();
+        idle.pop_back();
+        return 0;
+      }
+    }
+    std::unique_ptr<Ring> r(new Ring);
+    r->device = dev;
+    if (int rc = MakeRing(*r)) return rc;  // (the partial ring is freed by its destructor)
+    ring = r.release();
+    return 0;
+  }
+  // Back to the pool, or freed when kKeepIdle rings of this device are idle
+  // already.  The ring is quiescent here (every call drains its slots).
+  ~RingLease() {
+    if (ring == nullptr) return;
+    {
+      std::lock_guard<std::mutex> lk(Pool().mu);
+      std::vector<Ring*>& idle = Pool().idle[ring->device];
+      if (idle.size() < kKeepIdle) {
+        idle.push_back(ring);
+        return;
+      }
+    }
+    int cur = 0;
+    const int dev = ring->device;
+    (void)hipGetDevice(&cur);
+    if (cur != dev) (void)hipSetDevice(dev);
+    delete ring;
+    if (cur != dev) (void)hipSetDevice(cur);
   }
 };
-
-Ring* GetRing(int& rc) {
-  thread_local RingMap map;
-  std::map<int, std::unique_ptr<Ring>>& rings = map.rings;
-  int dev = 0;
-  hipGetDevice(&dev);
-  std::unique_ptr<Ring>& r = rings[dev];
-  if (!r) {
-    r.reset(new Ring);
-    rc = MakeRing(*r);
-    if (rc != 0) {
-      r.reset();
-      return nullptr;
-    }
-  }
-  rc = 0;
-  return r.get();
-}
 
 bool IsPinned(const void* p) {
   hipPointerAttribute_t a;
@@ -199,16 +235,17 @@ int leveldb_crc32c_batch_host(const void* host_base, const uint64_t* off, const 
     if (i && off[i] < off[i - 1]) return PipeFail(PRISMDB_CRC32C_EINVAL, "spans must be sorted by offset");
     if (off[i] < lead) return PipeFail(PRISMDB_CRC32C_EINVAL, "log record header before the buffer start");
   }
-  int rc = 0;
-  Ring* ring = GetRing(rc);
-  if (ring == nullptr) return rc;
+  RingLease lease;
+  int rc = lease.Acquire();
+  if (rc != 0) return rc;
+  Ring* const ring = lease.ring;
   const uint8_t* src = static_cast<const uint8_t*>(host_base);
   const bool pinned = IsPinned(host_base);
 
   // Abandon the call: wait for everything this call enqueued (DMAs may still
   // read the caller's source, kernels and D2H copies still write the slots)
   // and release every slot without copying anything out, so that the next
-  // call on this thread's ring starts empty.  Returns the original failure.
+  // call on this ring starts empty.  Returns the original failure.
   auto abort_call = [&](int code) -> int {
     const std::string msg = leveldb_crc32c_last_error();
     (void)hipStreamSynchronize(ring->copy);
@@ -272,7 +309,8 @@ int leveldb_crc32c_batch_host(const void* host_base, const uint64_t* off, const 
     if (e == hipSuccess) e = hipStreamWaitEvent(ring->compute, s.copied, 0);
     if (e != hipSuccess)
       return abort_call(PipeFail(PRISMDB_CRC32C_EDEVICE, std::string("pipeline H2D: ") + hipGetErrorString(e)));
-    rc = g_fail_after_chunks > 0 && ++chunks >= g_fail_after_chunks
+    const int fail_after = g_fail_after_chunks.load(std::memory_order_relaxed);
+    rc = fail_after > 0 && ++chunks >= fail_after
              ? PipeFail(PRISMDB_CRC32C_EDEVICE, "pipeline: injected failure (prismdb_pipeline_fail_after)")
              : leveldb_crc32c_batch(s.d_data, d_off, d_len, init ? d_init : nullptr, cnt, s.d_out,
                                     mismatch ? s.d_mm : nullptr, flags, ring->compute);
@@ -293,6 +331,6 @@ int leveldb_crc32c_batch_host(const void* host_base, const uint64_t* off, const 
   return 0;
 }
 
-void prismdb_pipeline_fail_after(int chunks) { g_fail_after_chunks = chunks > 0 ? chunks : 0; }
+void prismdb_pipeline_fail_after(int chunks) { g_fail_after_chunks.store(chunks > 0 ? chunks : 0, std::memory_order_relaxed); }
 
 }  // extern "C"

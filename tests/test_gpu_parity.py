@@ -652,9 +652,9 @@ def test_host_pipeline_mixed_large_spans(dev, oracle):
 
 
 def test_host_pipeline_failure_drains_ring(dev, oracle):
-    """A host batch that fails after several chunks are in flight leaves the
-    thread's ring empty: the next, smaller call on the same thread gets its own
-    results only and nothing is written past its output arrays."""
+    """A host batch that fails after several chunks are in flight returns its
+    ring to the pool empty: the next, smaller call (which leases it again)
+    gets its own results only and nothing is written past its output arrays."""
     import ctypes
 
     from prismdb_amd import _lib, crc32c
@@ -686,6 +686,39 @@ def test_host_pipeline_failure_drains_ring(dev, oracle):
     got, _ = crc32c.batch_host(host, off, lens)
     want, _ = oracle.batch(host, off, lens)
     np.testing.assert_array_equal(got, want)
+
+
+def test_host_pipeline_many_threads(dev, oracle):
+    """Host batches from 6 threads at once, then from 24 short-lived threads
+    (rings leased from the per-device pool, more concurrent calls than idle
+    rings kept): every call bit-exact, verify and mask mixed."""
+    import threading
+
+    from prismdb_amd import crc32c
+
+    n = 12000  # ~46 MiB: two chunks
+    off = np.arange(n, dtype=np.uint64) * 3992
+    lens = np.full(n, 3988, dtype=np.uint32)
+    host = oracle.synth(n * 3992 + 8, 0x5EED0011)
+    raw, _ = oracle.batch(host, off, lens)
+    masked, _ = oracle.batch(host, off, lens, mask=True)
+    errors = []
+
+    def run(t):
+        try:
+            got, _ = crc32c.batch_host(host, off, lens, mask=bool(t & 1))
+            if not (got == (masked if t & 1 else raw)).all():
+                errors.append(t)
+        except Exception as e:  # noqa: BLE001 - reported below
+            errors.append((t, repr(e)))
+
+    for first, count in ((0, 6), (6, 8), (14, 8), (22, 8)):
+        th = [threading.Thread(target=run, args=(first + t,)) for t in range(count)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join(120)
+    assert not errors, errors
 
 
 @pytest.fixture(params=["lane_all", "direct"])

@@ -1,17 +1,27 @@
 #!/usr/bin/env python3
-"""Compare compile-time variants of the engine in ONE process, interleaved.
+"""Compare variants of the engine in ONE process, interleaved.
 
-    python tools/variants.py build                 # here: build tools/_build/variants/*.so
-    python tools/variants.py run [--gib 64]        # GPU box: time them on one buffer
+    python tools/variants.py build [--only a b]     # here: build tools/_build/variants/lib_*.so
+    python tools/variants.py run [--gib 64] ...     # GPU box: time them on one buffer
 
-Each variant is the full library built with different -D knobs, loaded with
-RTLD_LOCAL and driven through its own C ABI (leveldb_crc32c_batch_fixed) on the
-same device buffer of 4 KiB blocks.  Results are also checked for equality.
+A variant is the full library built from a PATCHED COPY of the sources
+(tools/_build/variants/<name>/pkg/csrc): each entry of VARIANTS lists exact
+text substitutions (file, old, new), each of which must match exactly once.
+Measurement-only variants (marked "wrong results") exist only here, never as
+knobs in the product source.  Each library is loaded with RTLD_LOCAL and
+driven through its own C ABI on the same device buffer; results are compared
+across variants (`agree`).  Libraries built elsewhere (e.g. from an older
+commit in a git worktree) and dropped into VDIR as lib_<name>.so join the
+comparison with --only <name>.
+
+Earlier rounds' -D knob variants (profiles/r01_variants_*, r02*_variants_*)
+were measured with the knobs then in the source; those knobs are gone.
 """
 import argparse
 import ctypes
 import json
 import os
+import shutil
 import statistics
 import sys
 
@@ -19,100 +29,50 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 VDIR = os.path.join(ROOT, "tools", "_build", "variants")
 
+# Measurement-only variants compute wrong results on purpose: their device
+# self-test would refuse the device, so it is reported but not enforced.
+MEASURE_ONLY = [("crc32c_capi.hip", "  ctx.status = SelfTest(ctx);\n", "  (void)SelfTest(ctx);\n")]
+
+# name -> [(file under prismdb_amd/csrc, old text, new text), ...]
 VARIANTS = {
-    "base": {"PRISMDB_RING": 4, "PRISMDB_NT_LOADS": 1},
-    # measurement-only: fixed kernel without the CRC fold (loads + stores), wrong results
-    "nofold": {"PRISMDB_FIXED_NOFOLD": 1},
-    "nofold_nt0": {"PRISMDB_FIXED_NOFOLD": 1, "PRISMDB_NT_LOADS": 0},
-    "nostore": {"PRISMDB_FIXED_NOSTORE": 1},
-    "nofold_nostore": {"PRISMDB_FIXED_NOFOLD": 1, "PRISMDB_FIXED_NOSTORE": 1},
-    # measurement-only: span kernel folds rounds >= 12 / none (wrong results): the
-    # ceiling of skipping chunk 0's padding rounds on ~1 KB spans
-    "span_j12": {"PRISMDB_SPAN_J0": 12},
-    "span_j16": {"PRISMDB_SPAN_J0": 16},
-    # measurement-only: initial register always in round 0 (wrong where pad >= 64);
-    # snop: the s_nop 4 before the span kernel's buffer loads, as it was
-    "inj0": {"PRISMDB_SPAN_INJ0": 1},
-    # log-record kernel without the padding-round skip (straight 16-round fold)
-    "noskip": {"PRISMDB_LOG_ROUNDSKIP": 0},
-    "snop": {"PRISMDB_SPAN_SNOP": 1},
-    # fixed kernel: runs of 16 spans per wave instead of 64
-    "run3": {"PRISMDB_RUN_LG": 3},
-    # quad kernel (short records): measurement-only cuts (wrong results) and
-    # the realignment lookups in 2 groups / 1 group instead of 4
-    "quad_norealign": {"PRISMDB_QUAD_NOREALIGN": 1},
-    "quad_nomask": {"PRISMDB_QUAD_NOMASK": 1},
-    "quad_ra2": {"PRISMDB_QUAD_RALIGN_GROUPS": 2},
-    "quad_ra1": {"PRISMDB_QUAD_RALIGN_GROUPS": 1},
-    # quad kernel body loads: three address VALUs per load (clamped index)
-    "quad_clamped": {"PRISMDB_QUAD_CLAMPED": 1},
-    # quad kernel: unaligned body loads from the record's first byte (no head product)
-    "quad_unaligned": {"PRISMDB_QUAD_UNALIGNED": 1},
-    # (A/B helper: built from an older kernel source copied into the tree)
-    "older_src": {"PRISMDB_OLDER_SRC": 1},
-    # span kernel: initial register folded in (no ring-register copies at the merge)
-    "inj_fold": {"PRISMDB_SPAN_INJ_RING": 0},
-    # measurement-only: span kernel waits for every record's scalar read right away
-    "rec_wait": {"PRISMDB_SPAN_REC_WAIT": 1},
-    # measurement-only: fixed kernel with extra SALU / VALU per span pair (issue sensitivity)
-    "salu200": {"PRISMDB_FIXED_DUMMY_SALU": 200},
-    # span kernel: every group loads the tables, streams or not (as in round 1)
-    "no_wg_exit": {"PRISMDB_SPAN_WG_EXIT": 0},
-    # measurement-only: span kernel without its edge-byte load (desc4k stays exact: no tails)
-    "noedge": {"PRISMDB_SPAN_NOEDGE": 1, "PRISMDB_MEASURE_ONLY": 1},
-    # measurement: fixed kernel pairs spans half a run apart, like the span kernel's two streams
-    "far_pair": {"PRISMDB_FIXED_FAR_PAIR": 1},
-    # measurement: fixed kernel folds a pair as ONE dependent chain of 2K rounds (wrong results)
-    "chain": {"PRISMDB_FIXED_CHAIN": 1, "PRISMDB_MEASURE_ONLY": 1},
-    # fixed kernel: a pair's loads issued at wave priority 1 / 3 (s_setprio)
-    "setprio1": {"PRISMDB_FIXED_SETPRIO": 1},
-    "setprio3": {"PRISMDB_FIXED_SETPRIO": 3},
-    # span kernel: streams in their own runs even when every record is one task (round 1)
-    "no_pair_runs": {"PRISMDB_SPAN_PAIR_RUNS": 0},
-    # planner: a long span's thread writes its segment records alone (as in round 1)
-    "plan_serial": {"PRISMDB_PLAN_SERIAL_SEG": 1},
-    "valu64": {"PRISMDB_FIXED_DUMMY_VALU": 64},
-    # every descriptor batch through the quad kernel first
-    "quad_all": {"PRISMDB_QUAD_DEFAULT": 1},
-    # span kernel: at least 64 / 256 slices per record stream (finer tail balance)
-    "slices64": {"PRISMDB_SLICES_PER_STREAM": 64},
-    "slices256": {"PRISMDB_SLICES_PER_STREAM": 256},
-    # task-balanced slices: ceil(T / 2^lg) of them (round 1) instead of exactly m per stream
-    "slices_pow2": {"PRISMDB_SLICE_EXACT": 0},
-    # span kernel runs of 2^lg records (before the exact partition)
-    "runs_pow2": {"PRISMDB_RUNS_EXACT": 0},
-    # span kernel runs mode (one-task records): 16 runs per stream (round 1) / 256
-    "runs16": {"PRISMDB_RUNS_PER_STREAM": 16},
-    "runs256": {"PRISMDB_RUNS_PER_STREAM": 256},
-    # log batches through the quad kernel (four records per wave) instead of the lane kernel
-    "quadk": {"PRISMDB_LANE_KERNEL": 0},
-    # measurement-only: lane kernel loads without the fold (wrong results); the
-    # alignment / nt probes of profiles/r02s3f, r02s3h were knobs of earlier lane-kernel builds
-    "lane_nofold": {"PRISMDB_LANE_NOFOLD": 1, "PRISMDB_MEASURE_ONLY": 1},
-    # lane kernel with 8 / 4 waves per CU (fewer record lines in flight per CU)
-    "lane_w8": {"PRISMDB_LANE_THREADS": 512},
-    "lane_w12": {"PRISMDB_LANE_THREADS": 768},
-    "lane_w6": {"PRISMDB_LANE_THREADS": 384},
-    "lane_w10": {"PRISMDB_LANE_THREADS": 640},
-    "lane_w16": {"PRISMDB_LANE_THREADS": 1024},
-    "lane_w4": {"PRISMDB_LANE_THREADS": 256},
-    # quad kernel ring depth (tasks in flight + 1)
-    "quad_r2": {"PRISMDB_QUAD_RING": 2},
-    "quad_r3": {"PRISMDB_QUAD_RING": 3},
+    "base": [],
+    # an identical copy under another name: A/A check of the harness
+    "base2": [],
+    # measurement-only (wrong results): the one-launch kernel without its LDS
+    # table fill -- what the fill costs a file-sized call
+    "direct_notables": [("crc32c_direct.hip", "    load_tables<kDirectThreads>(lds, a.tabs, tid);\n", "")]
+    + MEASURE_ONLY,
+    # measurement-only (wrong results): the static ring without the table fold
+    # (loads, edges and stores only) -- what the fold costs
+    "direct_nofold": [("crc32c_direct.hip",
+                       "          for (int st = 0; st < 3; ++st) acc[st] = step256(lds, tab, acc[st], w[st][j]);",
+                       "          for (int st = 0; st < 3; ++st) acc[st] ^= w[st][j];")] + MEASURE_ONLY,
 }
-# Measured and dropped (profiles/r01_variants_ring_runs.json): refilling a ring
-# pair before its fold with a 6-buffer ring ("early6") was no faster.
-# Libraries built elsewhere (e.g. from an older commit in a git worktree) and
-# dropped into VDIR as lib_<name>.so join the comparison with --only <name>.
 
 
 def do_build(names):
-    from prismdb_amd.build import build
+    from prismdb_amd.build import CSRC, build
 
     for name in names:
         if name not in VARIANTS:
             continue
-        print(build(defines=VARIANTS[name], lib_path=os.path.join(VDIR, f"lib_{name}.so")))
+        vroot = os.path.join(ROOT, "build", "variants", name)  # sources and objects stay out of the GPU snapshot
+        src = os.path.join(vroot, "pkg", "csrc")
+        if os.path.isdir(src):
+            shutil.rmtree(src)
+        shutil.copytree(CSRC, src)
+        inc = os.path.join(vroot, "include")
+        if not os.path.exists(inc):
+            os.symlink(os.path.join(ROOT, "include"), inc)
+        for fname, old, new in VARIANTS[name]:
+            path = os.path.join(src, fname)
+            with open(path) as f:
+                text = f.read()
+            if text.count(old) != 1:
+                raise SystemExit(f"variant {name}: patch for {fname} matches {text.count(old)} times")
+            with open(path, "w") as f:
+                f.write(text.replace(old, new))
+        print(build(src_dir=src, obj_dir=os.path.join(vroot, "obj"), lib_path=os.path.join(VDIR, f"lib_{name}.so")))
 
 
 def do_run(args, names):
@@ -183,7 +143,8 @@ def do_run(args, names):
     foff = torch.from_numpy(np.concatenate([np.arange(nfd, dtype=np.int64) * 3992, [nfd * 3992]])).to(dev)
     flen = torch.from_numpy(np.concatenate([np.full(nfd, 3988, dtype=np.int32), [486977]]).astype(np.int32)).to(dev)
     fout = torch.empty(nfd + 1, dtype=torch.int32, device=dev)
-    calls = {"file_fixed": 50, "file_desc": 50}
+    fmm = torch.empty(nfd + 1, dtype=torch.uint8, device=dev)
+    calls = {"file_fixed": 50, "file_desc": 50, "file_verify": 50, "tiny_desc": 50}
     work = {
         "fixed4k": (lambda n: libs[n][0](buf.data_ptr(), 4096, 4096, nblk, 0, out.data_ptr(), None, 0, sp),
                     nblk * 4100),
@@ -210,6 +171,11 @@ def do_run(args, names):
                        nfd * (3988 + 4)),
         "file_desc": (lambda n: libs[n][1](buf.data_ptr(), foff.data_ptr(), flen.data_ptr(), None, nfd + 1,
                                            fout.data_ptr(), None, 0, sp), nfd * (3988 + 16) + 486977 + 16),
+        "file_verify": (lambda n: libs[n][1](buf.data_ptr(), foff.data_ptr(), flen.data_ptr(), None, nfd + 1,
+                                             fout.data_ptr(), fmm.data_ptr(), 0, sp), nfd * (3988 + 17) + 486977 + 17),
+        # one 4 KiB span: the per-call floor of the one-launch path
+        "tiny_desc": (lambda n: libs[n][1](buf.data_ptr(), off4k.data_ptr(), len4k.data_ptr(), None, 1,
+                                           fout.data_ptr(), None, 0, sp), 4096 + 16),
     }
 
     def timed(fn, n, k=1):  # mean of k back-to-back calls
@@ -226,7 +192,8 @@ def do_run(args, names):
         work = {w: v for w, v in work.items() if w in args.work}
     res = {w: {n: [] for n in names} for w in work}
     agree = {}
-    outs_of = {"wal": wout, "wal_seal": wout, "sst3988": sout, "huge64m": hout, "file_fixed": fout, "file_desc": fout}
+    outs_of = {"wal": wout, "wal_seal": wout, "sst3988": sout, "huge64m": hout, "file_fixed": fout, "file_desc": fout,
+               "file_verify": fout, "tiny_desc": fout}
     for w, (fn, _) in work.items():
         ref = None
         for n in names:
