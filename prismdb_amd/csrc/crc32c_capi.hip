@@ -389,9 +389,10 @@ int PlannerWorkspace(Workspace& w, hipStream_t s, size_t nspans, uint32_t stream
   return 0;
 }
 
-// The one-launch path's workspace: counters (zero between calls: the kernel's
-// last group resets them), the ticket map (entries carry the call's gen), the
-// partial registers and the per-span ticket counters (zero between calls).
+// The one-launch path's workspace: the two claim words (the call's, zero at
+// its start, and the next call's, which it zeroes), the ticket map (entries
+// carry the call's gen), the partial registers and the per-span ticket
+// counters (zero between calls: a span's combiner resets its own).
 int DirectWorkspace(Workspace& w, hipStream_t s, prismdb::dev::DirectWs* out) {
   namespace d = prismdb::dev;
   const size_t cap = d::kDirectTickets;
@@ -401,16 +402,24 @@ int DirectWorkspace(Workspace& w, hipStream_t s, prismdb::dev::DirectWs* out) {
     hipError_t e = hipMemsetAsync(w.direct, 0, bytes, s);
     if (e != hipSuccess) return FailHip(e, "ticket workspace memset");
   }
+  // Generations: map entries of earlier calls never match; `word` alternates
+  // between two slots by parity (each call zeroes the next call's).  At the
+  // wrap (2^32 calls) the workspace is zeroed again and the count restarts.
+  if (++w.gen == 0) {
+    hipError_t e = hipMemsetAsync(w.direct, 0, bytes, s);
+    if (e != hipSuccess) return FailHip(e, "ticket workspace memset");
+    w.gen = 1;
+  }
   char* p = w.direct;
-  out->word = reinterpret_cast<unsigned long long*>(p);
-  out->done = reinterpret_cast<uint32_t*>(p + 8);
+  out->word = reinterpret_cast<unsigned long long*>(p + 8 * (w.gen & 1u));
+  out->next = reinterpret_cast<unsigned long long*>(p + 8 * ((w.gen + 1u) & 1u));
   out->stats = reinterpret_cast<uint32_t*>(p + 16);
   out->tmap = reinterpret_cast<uint32_t*>(p + 256);
   out->part = reinterpret_cast<uint32_t*>(p + 256 + cap * 16);
   out->cdone = reinterpret_cast<uint32_t*>(p + 256 + cap * 20);
   out->cap = g_direct_cap.load(std::memory_order_relaxed);
   out->dbg = g_direct_dbg.load(std::memory_order_relaxed);
-  out->gen = ++w.gen == 0 ? ++w.gen : w.gen;  // 0 is the zeroed map's
+  out->gen = w.gen;  // 0 is the zeroed map's
   return 0;
 }
 

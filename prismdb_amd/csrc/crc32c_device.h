@@ -151,15 +151,15 @@ constexpr uint32_t kDirectTickets = 1u << 20;  // ticket workspace (beyond it: w
 constexpr uint32_t kNullSpan = 0xFFFFFFFFu;
 
 struct DirectWs {
-  unsigned long long* word;  // supply << 32 | claimed: tickets pushed / tickets taken
-  uint32_t* done;            // groups finished (the last one resets word and done)
+  unsigned long long* word;  // this call's supply << 32 | claimed: tickets pushed / tickets taken
+  unsigned long long* next;  // the next call's word (calls alternate; this call zeroes it)
   uint32_t* tmap;            // per ticket: span, its first ticket, T | lg << 24, gen
   uint32_t* part;            // per ticket: partial register
   uint32_t* cdone;           // per span, at its first ticket: tickets finished
   uint32_t* stats;           // cumulative: tickets adopted, spans folded whole, tickets claimed early / late
   uint32_t cap;              // tickets
   uint32_t gen;              // this call's generation: tmap entries of earlier calls never match
-  uint32_t dbg;              // test hook: bit 0 delays every push by ~100 us (claims run out first: orphans)
+  uint32_t dbg;              // test hooks: bit 0 delays every push by ~100 us, bit 1 blind worker claims
 };
 
 constexpr uint32_t kMaxPlanBlocks = 4096;

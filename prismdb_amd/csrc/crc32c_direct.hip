@@ -26,7 +26,7 @@
 //   workers      the last nwaves / 32 waves have no run (at most 256 of them:
 //                every worker reads `word`, and same-address reads serialize
 //                in one L2 channel, ~2.5 ns each).  A worker polls `word` for
-//                up to ~5 us, claims tickets one at a time while any are
+//                up to ~2 us, claims tickets one at a time while any are
 //                visible, and leaves.  A long span's chunks thus go out with
 //                the first loads instead of on the kernel's tail.
 //   late claims  a wave that pushed tickets claims, after its own run, one at
@@ -45,9 +45,11 @@
 // that finishes a span's last ticket (per-span counter) combines
 // R = sum_k M^(T-1-k) R_k, M = shift_{4 KiB g}, lane-parallel as
 // crc32c_combine_kernel does, feeds the tail bytes and stores the result.
-// The last group to finish resets `word` and the group counter for the next
-// call on the stream (the workspace is per (thread, device, stream)).  If the
-// ticket workspace is full, the discovering wave folds its long spans whole.
+// Calls on a stream (the workspace is per (thread, device, stream)) alternate
+// between two claim words: each call starts on a zeroed one and zeroes the
+// other for the next call -- no end-of-kernel counter (256 groups' atomics on
+// one address serialize in its L2 channel, ~35 ns each).  If the ticket
+// workspace is full, the discovering wave folds its long spans whole.
 // Test hooks (DirectWs::dbg): bit 0 delays every push by ~100 us, bit 1 makes
 // every worker claim once blindly (orphans); stats[] counts adopted tickets,
 // whole spans, worker claims and late claims.
@@ -127,6 +129,11 @@ __device__ __forceinline__ DTask geometry(uint64_t p, uint32_t len) {
 // tasks x 4 KiB in flight each, 72 MiB over the chip: a whole SST file's
 // reads are issued at once.
 constexpr uint32_t kDirectWaves = kDirectThreads / 64u;
+// How long a ticket worker polls `word`, in s_memrealtime ticks (100 MHz):
+// 2 us.  Workers are the grid's last waves, which start last: pushes come
+// right after the static waves' discovery, mostly before the workers run.
+// A push the workers miss is claimed by its pusher after its run.
+constexpr uint64_t kWorkerPoll = 200u;
 
 template <bool kVerify>
 __global__ __launch_bounds__(kDirectThreads) void crc32c_direct_kernel(SpanBatch a, DirectWs d) {
@@ -231,16 +238,15 @@ __global__ __launch_bounds__(kDirectThreads) void crc32c_direct_kernel(SpanBatch
     }
   }
 
-  // A group without static work, adopted tickets, whole spans or visible
-  // tickets leaves before loading the tables.  (The OR over the group goes
-  // through the table area: the tables take all of LDS.)
-  // (the reserved waves -- the last ones, whose groups start last -- stay for
-  // pushes still to come)
-  bool work = m != 0u || adopt_lo < adopt_hi || worker;
-  if (!work && lane == 0) {
-    const uint64_t wd = __hip_atomic_load(d.word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    work = (uint32_t)(wd >> 32) > (uint32_t)wd;
-  }
+  // The next call's claim word starts at zero (calls on a stream alternate
+  // between the two; nothing in this call touches the other one).
+  if (wave == 0 && lane == 0) __hip_atomic_store(d.next, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+
+  // A group without static work, adopted tickets, whole spans or workers
+  // leaves before loading the tables.  (The OR over the group goes through
+  // the table area: the tables take all of LDS.)  Idle waves do not look at
+  // `word`: thousands of reads of one address serialize in its L2 channel.
+  const bool work = m != 0u || adopt_lo < adopt_hi || worker;
   const bool wwork = __ballot(work) != 0u;
   if (lane == 0) lds[tid >> 6] = wwork ? 1u : 0u;
   __syncthreads();
@@ -249,8 +255,85 @@ __global__ __launch_bounds__(kDirectThreads) void crc32c_direct_kernel(SpanBatch
   for (int k = 0; k < (int)kDirectWaves; ++k) any |= lds[k];
   __syncthreads();
   if (any != 0u) {
-    load_tables<kDirectThreads>(lds, a.tabs, tid);
-    __syncthreads();
+    // ---- the static run's first loads go out before the table fill: the
+    // fill's own loads (one round trip) and its LDS writes then overlap the
+    // first data round trip instead of preceding it.
+    const uint64_t inrun = m >= 64u ? ~0ull : (1ull << m) - 1ull;
+    const uint64_t shortm = inrun & ~lm;
+    // next short span of stream st at or after position j
+    auto static_task = [&](uint32_t& j, uint32_t st) -> DTask {
+      const uint64_t par = 0x9249249249249249ull << st;  // positions st mod 3
+      const uint64_t from = j >= 64u ? 0ull : ~0ull << j;
+      const uint64_t avail = shortm & par & from;
+      if (avail == 0u) {
+        j = 64u;
+        DTask t = geometry(base, 0u);
+        t.f = 0;  // kind none
+        return t;
+      }
+      const uint32_t p = (uint32_t)__builtin_ctzll(avail);
+      const uint64_t off = ((uint64_t)readlane(voff_hi, p) << 32) | readlane(voff_lo, p);
+      DTask t = geometry(base + off, readlane(vlen, p));
+      t.b = sbase + p;
+      t.f |= (kKindStatic << 14) | (p << 17);
+      j = p + 3u;
+      return t;
+    };
+    // 17 loads per task, always: 16 body dwords (the buffer range check
+    // reads 0 outside the body: chunk 0's padding) and one edge byte per
+    // lane -- head bytes (lanes 0-2), tail bytes (3-5), stored crc (6-9).
+    auto issue = [&](const DTask& t, uint32_t (&w)[kRounds], uint32_t& e) {
+      const bool live = t.valid();
+      const uint32_t pad = t.pad(), h = t.h(), tl = t.t(), len = t.len();
+      const bool hwin = kVerify && hdr;
+      auto sat = [](uint64_t x) -> uint32_t { return x > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)x; };
+      const uint64_t start = t.body - h;
+      u32x4 rb = buffer_rsrc(reinterpret_cast<const uint8_t*>(t.body), live ? t.z : 0u);
+      u32x4 re = buffer_rsrc(reinterpret_cast<const uint8_t*>(hwin ? start - kLogCrcBack : start),
+                             live ? (hwin ? sat((uint64_t)kLogCrcBack + len) : sat((uint64_t)len + (kVerify ? 4u : 0u)))
+                                  : 0u);
+      // SGPRs the vector unit wrote (readlane) need 5 wait states before a
+      // VMEM instruction reads them; hipcc inserts none before inline asm.
+      asm volatile("s_nop 4" : "+s"(rb), "+s"(re));
+      const int32_t i0 = (int32_t)lane - (int32_t)pad;
+      if (pad == 0) {
+        load_rounds(w, rb, (uint32_t)i0 * 4u);
+      } else if (pad <= 64u) {
+        w[0] = buf_dword<0>(rb, (uint32_t)i0 * 4u);
+        load_rounds_from1(w, rb, (uint32_t)(i0 + 64) * 4u);
+      } else {
+#pragma unroll
+        for (int j = 0; j < kRounds; ++j) w[j] = buf_dword<0>(rb, (uint32_t)(i0 + 64 * j) * 4u);
+      }
+      const uint32_t hb = hwin ? kLogCrcBack : 0u;  // edge-window offset of the span's first byte
+      uint32_t eoff = 0xFFFFFFFFu;
+      if (lane < h) eoff = hb + lane;
+      if (lane >= 3u && lane < 3u + tl) eoff = sat((uint64_t)hb + h + t.z + (lane - 3u));
+      if (kVerify && lane >= 6u && lane < 10u) eoff = hwin ? lane - 6u : sat((uint64_t)len + (lane - 6u));
+      e = buf_ubyte(re, eoff);
+    };
+    DTask tk[2][3];
+    uint32_t wb[2][3][kRounds];
+    uint32_t eb[2][3];
+    uint32_t jc[3] = {0u, 1u, 2u};
+#pragma unroll
+    for (int sl = 0; sl < 2; ++sl) {
+#pragma unroll
+      for (int st = 0; st < 3; ++st) tk[sl][st] = static_task(jc[st], (uint32_t)st);  // (none without a run)
+    }
+    TableRegs<kDirectThreads> tr;
+    tables_issue(tr, a.tabs, tid);
+    // Every wave runs the ring (a wave without a run: empty tasks, whose
+    // range-checked loads touch no memory, and no folds), so the ring's
+    // registers have one definition on every path: hipCC then never copies
+    // an in-flight register at a merge (tools/check_inflight.py).
+#pragma unroll
+    for (int st = 0; st < 3; ++st) issue(tk[0][st], wb[0][st], eb[0][st]);
+    tables_wait<3 * (kRounds + 1)>(tr);  // slot 0's 51 loads stay in flight
+    tables_store<kDirectThreads>(lds, tr, tid);
+    // Group barrier for the LDS image.  Not __syncthreads(): its release
+    // fence waits for every outstanding load (vmcnt(0)), slot 0's included.
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     const StrideLanes tab = stride_lanes(lane);
     const uint32_t nibtab = 4u * (kTabWords + lane);
     const ShortShift ss = short_shift_cols(lane);
@@ -417,40 +500,6 @@ __global__ __launch_bounds__(kDirectThreads) void crc32c_direct_kernel(SpanBatch
       c = readlane((uint32_t)old, 0);
     };
 
-    // ---- early: this wave's orphans, its whole spans, up to two claims
-    for (uint32_t tkt = adopt_lo; tkt < adopt_hi; ++tkt) run_ticket(tkt);
-    for (uint64_t wm = whole; wm != 0u; wm &= wm - 1u) run_whole((uint32_t)__builtin_ctzll(wm));
-    // A worker waits up to ~5 us for the first push (bounded: nothing ever
-    // waits for another wave's progress), then claims tickets one at a time
-    // until none is left.  (All 2048 waves claiming at once after the table
-    // load serialized ~2048 atomics on one address, ~70 us.)
-    if (worker) {
-      if (d.dbg & 2u) {  // test hook: one blind claim (an orphan while nothing is pushed)
-        uint32_t c = 0, sp = 0;
-        claim(1u, c, sp);
-        if (c < sp) {
-          if (lane == 0) atomicAdd(d.stats + 2, 1u);
-          if (c < d.cap) run_ticket(c);
-        }
-      }
-      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-      for (;;) {
-        uint64_t wd = 0;
-        if (lane == 0) wd = __hip_atomic_load(d.word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const uint32_t S = readlane((uint32_t)(wd >> 32), 0), C = readlane((uint32_t)wd, 0);
-        if (S > C) {
-          uint32_t c = 0, sp = 0;
-          claim(1u, c, sp);
-          if (c >= sp) break;  // an orphan: its pusher does it
-          if (lane == 0) atomicAdd(d.stats + 2, 1u);
-          if (c < d.cap) run_ticket(c);
-          continue;
-        }
-        if (__builtin_amdgcn_s_memrealtime() - t0 > 500u) break;  // 100 MHz: 5 us
-        __builtin_amdgcn_s_sleep(32);
-      }
-    }
-
     // ---- the static run: one-chunk spans, stream st (of three) taking run
     // positions st, st + 3, ... (long ones skipped).  Ring of two slots x
     // three streams (six tasks, 102 loads in flight; a wait leaves the other
@@ -458,61 +507,7 @@ __global__ __launch_bounds__(kDirectThreads) void crc32c_direct_kernel(SpanBatch
     // loads, counted waits -- crc32c_span_kernel's ring with a third chain.
     // With 12 waves per CU, an SST file's ~5.6 spans per wave are all
     // requested at once.
-    if (m != 0u) {
-      const uint64_t inrun = m >= 64u ? ~0ull : (1ull << m) - 1ull;
-      const uint64_t shortm = inrun & ~lm;
-      // next short span of stream st at or after position j
-      auto static_task = [&](uint32_t& j, uint32_t st) -> DTask {
-        const uint64_t par = 0x9249249249249249ull << st;  // positions st mod 3
-        const uint64_t from = j >= 64u ? 0ull : ~0ull << j;
-        const uint64_t avail = shortm & par & from;
-        if (avail == 0u) {
-          j = 64u;
-          DTask t = geometry(base, 0u);
-          t.f = 0;  // kind none
-          return t;
-        }
-        const uint32_t p = (uint32_t)__builtin_ctzll(avail);
-        const uint64_t off = ((uint64_t)readlane(voff_hi, p) << 32) | readlane(voff_lo, p);
-        DTask t = geometry(base + off, readlane(vlen, p));
-        t.b = sbase + p;
-        t.f |= (kKindStatic << 14) | (p << 17);
-        j = p + 3u;
-        return t;
-      };
-      // 17 loads per task, always: 16 body dwords (the buffer range check
-      // reads 0 outside the body: chunk 0's padding) and one edge byte per
-      // lane -- head bytes (lanes 0-2), tail bytes (3-5), stored crc (6-9).
-      auto issue = [&](const DTask& t, uint32_t (&w)[kRounds], uint32_t& e) {
-        const bool live = t.valid();
-        const uint32_t pad = t.pad(), h = t.h(), tl = t.t(), len = t.len();
-        const bool hwin = kVerify && hdr;
-        auto sat = [](uint64_t x) -> uint32_t { return x > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)x; };
-        const uint64_t start = t.body - h;
-        u32x4 rb = buffer_rsrc(reinterpret_cast<const uint8_t*>(t.body), live ? t.z : 0u);
-        u32x4 re = buffer_rsrc(reinterpret_cast<const uint8_t*>(hwin ? start - kLogCrcBack : start),
-                               live ? (hwin ? sat((uint64_t)kLogCrcBack + len) : sat((uint64_t)len + (kVerify ? 4u : 0u)))
-                                    : 0u);
-        // SGPRs the vector unit wrote (readlane) need 5 wait states before a
-        // VMEM instruction reads them; hipcc inserts none before inline asm.
-        asm volatile("s_nop 4" : "+s"(rb), "+s"(re));
-        const int32_t i0 = (int32_t)lane - (int32_t)pad;
-        if (pad == 0) {
-          load_rounds(w, rb, (uint32_t)i0 * 4u);
-        } else if (pad <= 64u) {
-          w[0] = buf_dword<0>(rb, (uint32_t)i0 * 4u);
-          load_rounds_from1(w, rb, (uint32_t)(i0 + 64) * 4u);
-        } else {
-#pragma unroll
-          for (int j = 0; j < kRounds; ++j) w[j] = buf_dword<0>(rb, (uint32_t)(i0 + 64 * j) * 4u);
-        }
-        const uint32_t hb = hwin ? kLogCrcBack : 0u;  // edge-window offset of the span's first byte
-        uint32_t eoff = 0xFFFFFFFFu;
-        if (lane < h) eoff = hb + lane;
-        if (lane >= 3u && lane < 3u + tl) eoff = sat((uint64_t)hb + h + t.z + (lane - 3u));
-        if (kVerify && lane >= 6u && lane < 10u) eoff = hwin ? lane - 6u : sat((uint64_t)len + (lane - 6u));
-        e = buf_ubyte(re, eoff);
-      };
+    {
       auto fold = [&](const DTask (&t)[3], uint32_t (&w)[3][kRounds], const uint32_t (&e)[3]) {
         uint32_t r[3], acc[3] = {0u, 0u, 0u};
 #pragma unroll
@@ -536,21 +531,10 @@ __global__ __launch_bounds__(kDirectThreads) void crc32c_direct_kernel(SpanBatch
           if (t[st].valid()) finish(t[st], t[st].z ? bv : r[st], edge_tail(e[st], t[st].t()), edge_stored(e[st]), true);
         }
       };
-      DTask tk[2][3];
-      uint32_t wb[2][3][kRounds];
-      uint32_t eb[2][3];
-      uint32_t jc[3] = {0u, 1u, 2u};
+      {
+        // slot 0 went out before the table fill; slot 1 now
 #pragma unroll
-      for (int sl = 0; sl < 2; ++sl) {
-#pragma unroll
-        for (int st = 0; st < 3; ++st) tk[sl][st] = static_task(jc[st], (uint32_t)st);
-      }
-      if (tk[0][0].valid() || tk[0][1].valid() || tk[0][2].valid()) {
-#pragma unroll
-        for (int sl = 0; sl < 2; ++sl) {
-#pragma unroll
-          for (int st = 0; st < 3; ++st) issue(tk[sl][st], wb[sl][st], eb[sl][st]);
-        }
+        for (int st = 0; st < 3; ++st) issue(tk[1][st], wb[1][st], eb[1][st]);
         constexpr int kYounger = 3 * (kRounds + 1);  // the other slot's three tasks
         static_assert(kYounger <= 63, "vmcnt counts at most 63 loads");
         for (;;) {
@@ -558,7 +542,7 @@ __global__ __launch_bounds__(kDirectThreads) void crc32c_direct_kernel(SpanBatch
           for (int sl = 0; sl < 2; ++sl) {
 #pragma unroll
             for (int st = 0; st < 3; ++st) wait_task<kYounger>(wb[sl][st], eb[sl][st]);
-            fold(tk[sl], wb[sl], eb[sl]);
+            if (tk[sl][0].valid() || tk[sl][1].valid() || tk[sl][2].valid()) fold(tk[sl], wb[sl], eb[sl]);
             if (!tk[sl ^ 1][0].valid() && !tk[sl ^ 1][1].valid() && !tk[sl ^ 1][2].valid()) goto drained;
 #pragma unroll
             for (int st = 0; st < 3; ++st) tk[sl][st] = static_task(jc[st], (uint32_t)st);
@@ -574,6 +558,42 @@ __global__ __launch_bounds__(kDirectThreads) void crc32c_direct_kernel(SpanBatch
         }
       }
     }
+
+    // ---- workers
+    // A worker polls for pushes for a bounded time (nothing ever waits for
+    // another wave's progress) and claims visible tickets one at a time.  (All 2048 waves claiming at once after the table
+    // load serialized ~2048 atomics on one address, ~70 us.)
+    if (worker) {
+      if (d.dbg & 2u) {  // test hook: one blind claim (an orphan while nothing is pushed)
+        uint32_t c = 0, sp = 0;
+        claim(1u, c, sp);
+        if (c < sp) {
+          if (lane == 0) atomicAdd(d.stats + 2, 1u);
+          if (c < d.cap) run_ticket(c);
+        }
+      }
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      for (;;) {
+        uint64_t wd = 0;
+        if (lane == 0) wd = __hip_atomic_load(d.word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t S = readlane((uint32_t)(wd >> 32), 0), C = readlane((uint32_t)wd, 0);
+        if (S > C) {
+          uint32_t c = 0, sp = 0;
+          claim(1u, c, sp);
+          if (c >= sp) break;  // an orphan: its pusher does it
+          if (lane == 0) atomicAdd(d.stats + 2, 1u);
+          if (c < d.cap) run_ticket(c);
+          continue;
+        }
+        if (__builtin_amdgcn_s_memrealtime() - t0 > kWorkerPoll) break;
+        __builtin_amdgcn_s_sleep(32);
+      }
+    }
+
+    // ---- after the run (rare: a push that found its tickets claimed, or a
+    // full ticket workspace): this wave's orphans and its whole spans
+    for (uint32_t tkt = adopt_lo; tkt < adopt_hi; ++tkt) run_ticket(tkt);
+    for (uint64_t wm = whole; wm != 0u; wm &= wm - 1u) run_whole((uint32_t)__builtin_ctzll(wm));
 
     // ---- late: a wave that pushed tickets claims, one at a time, until
     // none is left -- its own included, whoever else did not take them, so
@@ -598,15 +618,6 @@ __global__ __launch_bounds__(kDirectThreads) void crc32c_direct_kernel(SpanBatch
     }
   }
 
-  // The last group to finish resets the counters for the next call.
-  __syncthreads();
-  if (tid == 0) {
-    const uint32_t old = __hip_atomic_fetch_add(d.done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    if (old + 1u == gridDim.x) {
-      __hip_atomic_store(d.word, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(d.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
 }
 
 hipError_t launch_direct(const SpanBatch& a, bool verify, int grid, const DirectWs& d, hipStream_t s) {

@@ -123,28 +123,64 @@ __device__ __forceinline__ StrideLanes stride_lanes(uint32_t lane) {
 // a wave 256 B apart -- all on the same four banks -- and took ~4 us per
 // group; one LDS word per thread, round 2's fill, needs 4x the instructions.)
 // The table words come from L1 (eight lanes read each).  The per-lane nibble
-// tables (32 KiB) are copied 16 B per lane, also consecutive.
+// tables (32 KiB) are copied 16 B per lane, also consecutive.  Every global
+// load of a thread is issued before its first LDS store (one memory round trip
+// per group at kernel start instead of one per loop step: the fill sits in
+// front of every kernel's first data load).
 template <int kT>
 __device__ __forceinline__ void load_stride_image(uint32_t* lds, const uint32_t* tab, uint32_t tid) {
   typedef uint32_t v4 __attribute__((ext_vector_type(4)));
+  constexpr int kS = (8192 + kT - 1) / kT;
   v4* dst = reinterpret_cast<v4*>(lds);
-#pragma unroll 4
-  for (uint32_t x = tid; x < 8192u; x += kT) {
+  uint32_t v[kS];
+#pragma unroll
+  for (int i = 0; i < kS; ++i) {
+    const uint32_t x = tid + (uint32_t)(i * kT);
     const uint32_t q = x >> 3;
     const uint32_t k = ((q >> 9) << 1) | (q & 1u), e = (q >> 1) & 255u;
-    const uint32_t v = tab[k * 256u + e];
-    const v4 w = {v, v, v, v};
-    dst[x] = w;
+    v[i] = (kS * kT == 8192 || x < 8192u) ? tab[k * 256u + e] : 0u;
+  }
+#pragma unroll
+  for (int i = 0; i < kS; ++i) {
+    const uint32_t x = tid + (uint32_t)(i * kT);
+    if (kS * kT == 8192 || x < 8192u) dst[x] = v4{v[i], v[i], v[i], v[i]};
   }
 }
 
 template <int kT = kThreads>
 __device__ __forceinline__ void load_tables(uint32_t* lds, const DeviceTables* tabs, uint32_t tid) {
   typedef uint32_t v4 __attribute__((ext_vector_type(4)));
-  load_stride_image<kT>(lds, &tabs->stride[0][0], tid);
+  constexpr int kS = (8192 + kT - 1) / kT;
+  constexpr uint32_t kNib = (uint32_t)kNibWords / 4u;
+  constexpr int kN = (int)((kNib + kT - 1) / kT);
+  const uint32_t* tab = &tabs->stride[0][0];
   const v4* nib = reinterpret_cast<const v4*>(&tabs->lane_nib[0][0][0]);
-  v4* dst = reinterpret_cast<v4*>(lds + kTabWords);
-  for (uint32_t e = tid; e < (uint32_t)kNibWords / 4u; e += kT) dst[e] = nib[e];
+  uint32_t v[kS];
+  v4 u[kN];
+#pragma unroll
+  for (int i = 0; i < kS; ++i) {
+    const uint32_t x = tid + (uint32_t)(i * kT);
+    const uint32_t q = x >> 3;
+    const uint32_t k = ((q >> 9) << 1) | (q & 1u), e = (q >> 1) & 255u;
+    v[i] = (kS * kT == 8192 || x < 8192u) ? tab[k * 256u + e] : 0u;
+  }
+#pragma unroll
+  for (int i = 0; i < kN; ++i) {
+    const uint32_t e = tid + (uint32_t)(i * kT);
+    u[i] = ((uint32_t)kN * kT == kNib || e < kNib) ? nib[e] : v4{0u, 0u, 0u, 0u};
+  }
+  v4* dst = reinterpret_cast<v4*>(lds);
+#pragma unroll
+  for (int i = 0; i < kS; ++i) {
+    const uint32_t x = tid + (uint32_t)(i * kT);
+    if (kS * kT == 8192 || x < 8192u) dst[x] = v4{v[i], v[i], v[i], v[i]};
+  }
+  v4* ndst = reinterpret_cast<v4*>(lds + kTabWords);
+#pragma unroll
+  for (int i = 0; i < kN; ++i) {
+    const uint32_t e = tid + (uint32_t)(i * kT);
+    if ((uint32_t)kN * kT == kNib || e < kNib) ndst[e] = u[i];
+  }
 }
 
 __device__ __forceinline__ uint32_t lds_word(const uint32_t* lds, uint32_t byte_addr) {
@@ -283,6 +319,71 @@ __device__ __forceinline__ uint32_t buf_ubyte(u32x4 rs, uint32_t voff) {
   uint32_t r;
   asm volatile("buffer_load_ubyte %0, %1, %2, 0 offen" : "=v"(r) : "v"(voff), "s"(rs));
   return r;
+}
+
+// The one-launch kernel's table fill in two halves, so that a wave's first
+// data loads can be issued between them: `issue` puts every table word this
+// thread copies into registers with inline-asm buffer loads (one round trip;
+// offsets past a table read 0, so no lane branches), the caller retires them
+// with a counted wait (tables_wait: the data loads issued after them stay in
+// flight), and `store` writes the LDS image load_tables writes.
+template <int kT>
+struct TableRegs {
+  static constexpr int kS = (8192 + kT - 1) / kT;
+  static constexpr int kN = (kNibWords / 4 + kT - 1) / kT;
+  uint32_t v[kS];
+  u32x4 u[kN];
+};
+
+template <int kT>
+__device__ __forceinline__ void tables_issue(TableRegs<kT>& r, const DeviceTables* tabs, uint32_t tid) {
+  u32x4 rs = buffer_rsrc(reinterpret_cast<const uint8_t*>(&tabs->stride[0][0]), 4u * 4u * 256u);
+  u32x4 rn = buffer_rsrc(reinterpret_cast<const uint8_t*>(&tabs->lane_nib[0][0][0]), 4u * (uint32_t)kNibWords);
+  // SGPRs the vector unit wrote (readfirstlane) need 5 wait states before a
+  // VMEM instruction reads them; hipcc inserts none before inline asm.
+  asm volatile("s_nop 4" : "+s"(rs), "+s"(rn));
+#pragma unroll
+  for (int i = 0; i < TableRegs<kT>::kS; ++i) {
+    const uint32_t x = tid + (uint32_t)(i * kT);
+    const uint32_t q = x >> 3;
+    const uint32_t k = ((q >> 9) << 1) | (q & 1u), e = (q >> 1) & 255u;
+    const uint32_t off = x < 8192u ? 4u * (k * 256u + e) : 0xFFFFFFF0u;
+    asm volatile("buffer_load_dword %0, %1, %2, 0 offen" : "=v"(r.v[i]) : "v"(off), "s"(rs));
+  }
+#pragma unroll
+  for (int i = 0; i < TableRegs<kT>::kN; ++i) {
+    const uint32_t e = tid + (uint32_t)(i * kT);
+    const uint32_t off = e < (uint32_t)kNibWords / 4u ? 16u * e : 0xFFFFFFF0u;
+    asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(r.u[i]) : "v"(off), "s"(rn));
+  }
+}
+
+// Retire the table loads with kYounger (data) loads left in flight.
+template <int kYounger>
+__device__ __forceinline__ void tables_wait(TableRegs<768>& r) {
+  static_assert(TableRegs<768>::kS == 11 && TableRegs<768>::kN == 3, "operand list below");
+  asm volatile("s_waitcnt vmcnt(%14)"
+               : "+v"(r.v[0]), "+v"(r.v[1]), "+v"(r.v[2]), "+v"(r.v[3]), "+v"(r.v[4]), "+v"(r.v[5]),
+                 "+v"(r.v[6]), "+v"(r.v[7]), "+v"(r.v[8]), "+v"(r.v[9]), "+v"(r.v[10]), "+v"(r.u[0]),
+                 "+v"(r.u[1]), "+v"(r.u[2])
+               : "n"(kYounger));
+}
+
+template <int kT>
+__device__ __forceinline__ void tables_store(uint32_t* lds, const TableRegs<kT>& r, uint32_t tid) {
+  typedef uint32_t v4 __attribute__((ext_vector_type(4)));
+  v4* dst = reinterpret_cast<v4*>(lds);
+#pragma unroll
+  for (int i = 0; i < TableRegs<kT>::kS; ++i) {
+    const uint32_t x = tid + (uint32_t)(i * kT);
+    if (x < 8192u) dst[x] = v4{r.v[i], r.v[i], r.v[i], r.v[i]};
+  }
+  v4* ndst = reinterpret_cast<v4*>(lds + kTabWords);
+#pragma unroll
+  for (int i = 0; i < TableRegs<kT>::kN; ++i) {
+    const uint32_t e = tid + (uint32_t)(i * kT);
+    if (e < (uint32_t)kNibWords / 4u) ndst[e] = v4{r.u[i].x, r.u[i].y, r.u[i].z, r.u[i].w};
+  }
 }
 
 // w[j] = round j at voff + 256 j, j = J..N-1 (immediate offsets).
