@@ -303,8 +303,10 @@ def config5_leg(args, torch, dist, crc32c, dev, rank, world) -> dict:
     compaction verifies its inputs block by block, table/format.cc:91-102),
     then (N > 1) one RCCL gather of the partition's 4-byte results to rank 0.
     Seal = MASK | WRITE_TRAILER (trailers written in place), verify = the
-    mismatch vector.  GiB/s of span bytes, whole job (all ranks), max-over-
-    ranks timing between barriers.  Checks: verify after seal flags nothing
+    mismatch vector; consecutive file calls carry PRISMDB_CRC32C_UNORDERED
+    (the files are disjoint), and the seal is also timed in stream order.
+    GiB/s of span bytes, whole job (all ranks), max-over-ranks timing
+    between barriers.  Checks: verify after seal flags nothing
     and returns the unmasked seal results; 256 spans of file 0 against the
     host leveldb_crc32c_value; the gathered digests."""
     import numpy as np
@@ -332,24 +334,24 @@ def config5_leg(args, torch, dist, crc32c, dev, rank, world) -> dict:
     sp = int(stream.cuda_stream)
     base, op, lp = buf.data_ptr(), d_off.data_ptr(), d_len.data_ptr()
 
-    def run(verify):
+    def run(verify, unordered):
         o = raw.data_ptr() if verify else out.data_ptr()
+        fl = (0 if verify else 0x3) | (0x8 if unordered else 0)  # seal: MASK | WRITE_TRAILER; 0x8: UNORDERED
         for f in range(nfiles):
             rc = L.leveldb_crc32c_batch(base + f * fbytes, op, lp, None, spf, o + 4 * f * spf,
-                                        (mm.data_ptr() + f * spf) if verify else None,
-                                        0 if verify else 0x3, sp)  # seal: MASK | WRITE_TRAILER
+                                        (mm.data_ptr() + f * spf) if verify else None, fl, sp)
             if rc != 0:
                 raise RuntimeError(f"leveldb_crc32c_batch: {L.leveldb_crc32c_last_error().decode()}")
 
     shard = ShardedBatch(nblocks_per_rank=n, block_bytes=0, rank=rank, world=world, device=dev, slots=1) \
         if world > 1 else None
 
-    def leg(verify):
+    def leg(verify, unordered=True):
         res = out if not verify else raw
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
               for _ in range(args.c5_steps)]
         for _ in range(2):
-            run(verify)
+            run(verify, unordered)
             if shard:
                 shard.gather_async(res, 0).wait()
         torch.cuda.synchronize()
@@ -359,7 +361,7 @@ def config5_leg(args, torch, dist, crc32c, dev, rank, world) -> dict:
         t0 = time.perf_counter()
         for i in range(args.c5_steps):
             ev[i][0].record(stream)
-            run(verify)
+            run(verify, unordered)
             ev[i][1].record(stream)
             if shard:
                 shard.gather_async(res, 0).wait()
@@ -383,6 +385,7 @@ def config5_leg(args, torch, dist, crc32c, dev, rank, world) -> dict:
 
     seal = leg(False)
     verify = leg(True)
+    seal_ordered = leg(False, unordered=False)
     torch.cuda.synchronize()
     bad = int(mm.sum().item())
     unmasked = (out.to(torch.int64) & 0xFFFFFFFF) - 0xA282EAD8
@@ -400,7 +403,9 @@ def config5_leg(args, torch, dist, crc32c, dev, rank, world) -> dict:
                      "leveldb_crc32c_batch per file" + (", RCCL gather of the results to rank 0" if world > 1 else "")),
         "files_per_gpu": nfiles, "spans_per_gpu": n, "span_bytes_per_gpu": nfiles * span_bytes,
         "steps": args.c5_steps, "scaling": "weak",
-        "seal": seal, "verify": verify,
+        "seal": seal, "verify": verify, "seal_ordered": seal_ordered,
+        "note": ("seal / verify: consecutive file calls flagged PRISMDB_CRC32C_UNORDERED (the files are disjoint: "
+                 "every other launch may overlap its predecessor); seal_ordered: the same calls in stream order"),
         "checks": {"verify_after_seal_mismatches": bad, "verify_equals_unmasked_seal": same,
                    "host_value_256_spans_file0": host_ok},
     }

@@ -52,6 +52,15 @@ extern "C" {
  * Mask(Extend(type_crc[t], payload)) == Mask(Value(type||payload));
  * db/log_reader.cc:231-245 checks Value(header + 6, 1 + length)). */
 #define PRISMDB_CRC32C_LOG_HEADER 0x4u
+/* leveldb_crc32c_batch (batch_fixed and batch_multi accept and ignore it,
+ * batch_host rejects it): this batch
+ * may start before the batch issued just before it on the same stream has
+ * finished -- the caller promises the two touch disjoint bytes (e.g. two SST
+ * files a compaction seals one after the other: table/table_builder.cc:206-261
+ * per file).  Consecutive UNORDERED batches alternate with ordered launches,
+ * so at most two batches of a stream are in flight.  Everything else keeps
+ * stream order: a later batch without the flag waits for both. */
+#define PRISMDB_CRC32C_UNORDERED 0x8u
 
 /* error codes */
 #define PRISMDB_CRC32C_EINVAL (-1)  /* bad argument */

@@ -32,6 +32,7 @@ kMaskDelta = 0xA282EAD8
 FLAG_MASK = 0x1
 FLAG_WRITE_TRAILER = 0x2
 FLAG_LOG_HEADER = 0x4
+FLAG_UNORDERED = 0x8
 
 
 def _bytes(data) -> bytes:
@@ -124,7 +125,7 @@ def _span_reach(log_header: bool, verify: bool, trailer: bool) -> Tuple[int, int
 
 def batch(buf, off, lens, init=None, *, mask: bool = False, verify: bool = False, out=None,
           mismatch=None, stream=None, trailer: bool = False, log_header: bool = False,
-          check_bounds: bool = True) -> Tuple[object, Optional[object]]:
+          check_bounds: bool = True, unordered: bool = False) -> Tuple[object, Optional[object]]:
     """CRC32C of arbitrary spans buf[off[i] : off[i]+lens[i]] (int64 off, int32 lens, int32 init).
 
     trailer=True also stores each (masked, with mask=True) result as 4 LE bytes
@@ -135,7 +136,11 @@ def batch(buf, off, lens, init=None, *, mask: bool = False, verify: bool = False
     fault).  The check is one device reduction and a host sync, so with the
     default the call blocks the host even when `stream` is given; callers
     that reuse descriptors they have already checked pass False and stay
-    asynchronous."""
+    asynchronous.
+
+    unordered: PRISMDB_CRC32C_UNORDERED -- this batch may overlap the batch
+    issued just before it on the stream (the caller promises they touch
+    disjoint bytes, e.g. consecutive SST files of a compaction)."""
     if trailer and verify:
         raise ValueError("trailer and verify are exclusive")
     torch = _torch()
@@ -164,7 +169,8 @@ def batch(buf, off, lens, init=None, *, mask: bool = False, verify: bool = False
     rc = lib().leveldb_crc32c_batch(
         buf.data_ptr(), off.data_ptr(), lens.data_ptr(), init.data_ptr() if init is not None else None, n,
         out.data_ptr(), mismatch.data_ptr() if verify else None,
-        (FLAG_MASK if mask else 0) | (FLAG_WRITE_TRAILER if trailer else 0) | (FLAG_LOG_HEADER if log_header else 0),
+        (FLAG_MASK if mask else 0) | (FLAG_WRITE_TRAILER if trailer else 0) | (FLAG_LOG_HEADER if log_header else 0)
+        | (FLAG_UNORDERED if unordered else 0),
         _stream_ptr(stream))
     check(rc, "leveldb_crc32c_batch")
     return out, (mismatch if verify else None)

@@ -228,7 +228,11 @@ int GetCtx(DeviceCtx** out) {
 struct Workspace {
   int device = -1;
   hipStream_t stream = nullptr;
-  hipEvent_t done = nullptr;  // recorded on `stream` after every batch that used the workspace
+  // Completion of the last batch of each slot parity (the one-launch path's
+  // calls alternate between two slots; the planner path marks done[gen & 1]):
+  // waiting for both covers everything that used the workspace.
+  hipEvent_t done[2] = {nullptr, nullptr};
+  bool prev_any = false;  // the last one-launch call was an any-order launch
   void* mem = nullptr;
   char* grow = nullptr;
   size_t cap_rec = 0;
@@ -249,11 +253,12 @@ constexpr size_t kMaxWorkspaces = 8;
 // the default pool so the memory leaves the process's pool too.
 void SyncAndRelease(Workspace& w) {
   if (t_last_counters == w.ws.counters) t_last_counters = nullptr;
-  if (w.direct != nullptr && t_last_stats == reinterpret_cast<const uint32_t*>(w.direct + 16)) t_last_stats = nullptr;
+  if (w.direct != nullptr && t_last_stats == reinterpret_cast<const uint32_t*>(w.direct + 32)) t_last_stats = nullptr;
   int cur = 0;
   (void)hipGetDevice(&cur);
   if (w.device != cur) (void)hipSetDevice(w.device);
-  if (w.done != nullptr) (void)hipEventSynchronize(w.done);
+  for (hipEvent_t ev : w.done)
+    if (ev != nullptr) (void)hipEventSynchronize(ev);
   const hipStream_t rs = g_ctx[w.device].release;
   for (void* blk : {static_cast<void*>(w.mem), static_cast<void*>(w.grow), static_cast<void*>(w.qgrow),
                     static_cast<void*>(w.direct)})
@@ -261,7 +266,8 @@ void SyncAndRelease(Workspace& w) {
   (void)hipStreamSynchronize(rs);
   hipMemPool_t pool = nullptr;
   if (hipDeviceGetDefaultMemPool(&pool, w.device) == hipSuccess) (void)hipMemPoolTrimTo(pool, 0);
-  if (w.done != nullptr) (void)hipEventDestroy(w.done);
+  for (hipEvent_t ev : w.done)
+    if (ev != nullptr) (void)hipEventDestroy(ev);
   if (w.device != cur) (void)hipSetDevice(cur);
   w = Workspace{};
 }
@@ -314,10 +320,12 @@ Workspace* FindWorkspace(hipStream_t s, int& rc) {
   w.stream = s;
   const size_t bytes = 256 + kCapSeg * (16 + 4) + (size_t)kCapLong * (8 + 8 + 4) +
                        (size_t)prismdb::dev::kMaxPlanBlocks * 8;
-  e = hipEventCreateWithFlags(&w.done, hipEventDisableTiming);
+  e = hipEventCreateWithFlags(&w.done[0], hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&w.done[1], hipEventDisableTiming);
   if (e == hipSuccess) e = hipMallocAsync(&w.mem, bytes, s);
   if (e != hipSuccess) {
-    if (w.done != nullptr) (void)hipEventDestroy(w.done);
+    for (hipEvent_t ev : w.done)
+      if (ev != nullptr) (void)hipEventDestroy(ev);
     lru.pop_front();
     rc = FailHip(e, "workspace allocation");
     return nullptr;
@@ -389,34 +397,39 @@ int PlannerWorkspace(Workspace& w, hipStream_t s, size_t nspans, uint32_t stream
   return 0;
 }
 
-// The one-launch path's workspace: the two claim words (the call's, zero at
-// its start, and the next call's, which it zeroes), the ticket map (entries
-// carry the call's gen), the partial registers and the per-span ticket
-// counters (zero between calls: a span's combiner resets its own).
+// The one-launch path's workspace: four claim words (call g uses word g % 4
+// and zeroes word (g + 2) % 4 for the call after next; at most two calls of a
+// stream are in flight, PRISMDB_CRC32C_UNORDERED), the usage counters, and
+// two slots (call parity) of: the ticket map (32-B entries carrying the
+// call's gen), the partial registers and the per-span ticket counters (zero
+// between calls: a span's combiner resets its own).
 int DirectWorkspace(Workspace& w, hipStream_t s, prismdb::dev::DirectWs* out) {
   namespace d = prismdb::dev;
   const size_t cap = d::kDirectTickets;
-  const size_t bytes = 256 + cap * (16 + 4 + 4);
+  const size_t slot_bytes = cap * (32 + 4 + 4);
+  const size_t bytes = 256 + 2 * slot_bytes;
   if (w.direct == nullptr) {
     if (int rc = GrowBlock(&w.direct, bytes, s, "ticket workspace")) return rc;
     hipError_t e = hipMemsetAsync(w.direct, 0, bytes, s);
     if (e != hipSuccess) return FailHip(e, "ticket workspace memset");
   }
-  // Generations: map entries of earlier calls never match; `word` alternates
-  // between two slots by parity (each call zeroes the next call's).  At the
-  // wrap (2^32 calls) the workspace is zeroed again and the count restarts.
+  // Generations: map entries of earlier calls never match.  At the wrap
+  // (2^32 calls) the workspace is zeroed again (an ordered command: behind
+  // both slots' last calls) and the count restarts.
   if (++w.gen == 0) {
     hipError_t e = hipMemsetAsync(w.direct, 0, bytes, s);
     if (e != hipSuccess) return FailHip(e, "ticket workspace memset");
     w.gen = 1;
+    w.prev_any = false;
   }
   char* p = w.direct;
-  out->word = reinterpret_cast<unsigned long long*>(p + 8 * (w.gen & 1u));
-  out->next = reinterpret_cast<unsigned long long*>(p + 8 * ((w.gen + 1u) & 1u));
-  out->stats = reinterpret_cast<uint32_t*>(p + 16);
-  out->tmap = reinterpret_cast<uint32_t*>(p + 256);
-  out->part = reinterpret_cast<uint32_t*>(p + 256 + cap * 16);
-  out->cdone = reinterpret_cast<uint32_t*>(p + 256 + cap * 20);
+  out->word = reinterpret_cast<unsigned long long*>(p + 8 * (w.gen & 3u));
+  out->next = reinterpret_cast<unsigned long long*>(p + 8 * ((w.gen + 2u) & 3u));
+  out->stats = reinterpret_cast<uint32_t*>(p + 32);
+  char* sl = p + 256 + (size_t)(w.gen & 1u) * slot_bytes;
+  out->tmap = reinterpret_cast<uint32_t*>(sl);
+  out->part = reinterpret_cast<uint32_t*>(sl + cap * 32);
+  out->cdone = reinterpret_cast<uint32_t*>(sl + cap * 36);
   out->cap = g_direct_cap.load(std::memory_order_relaxed);
   out->dbg = g_direct_dbg.load(std::memory_order_relaxed);
   out->gen = w.gen;  // 0 is the zeroed map's
@@ -432,6 +445,8 @@ enum Route { kRouteAuto = 0, kRouteDirect = 1, kRoutePlanner = 2 };
 // list in front for log-record batches.
 int RunBatch(DeviceCtx& ctx, const SpanBatch& base_args, bool desc, bool verify, hipStream_t s, int route) {
   SpanBatch a = base_args;
+  const bool unordered = (a.flags & PRISMDB_CRC32C_UNORDERED) != 0;  // host-side only
+  a.flags &= ~PRISMDB_CRC32C_UNORDERED;
   a.tabs = ctx.tabs;
   a.role = prismdb::dev::kRoleSpans;
   // Fast path: fixed stride, 4-byte aligned, 4..4096-byte multiple-of-4 spans
@@ -449,11 +464,20 @@ int RunBatch(DeviceCtx& ctx, const SpanBatch& base_args, bool desc, bool verify,
   int rc = 0;
   Workspace* w = FindWorkspace(s, rc);
   if (w == nullptr) return rc;
-  // whatever follows, the workspace's event marks the end of this call's work
+  // Whatever follows, the workspace's events mark the end of this call's
+  // work: the one-launch kernel's own completion (hipExtLaunchKernel's stop
+  // event), or a marker after the planner path's last launch (ordered: it
+  // covers everything before it).
   struct MarkDone {
     Workspace* w;
     hipStream_t s;
-    ~MarkDone() { (void)hipEventRecord(w->done, s); }
+    bool by_launch = false;
+    ~MarkDone() {
+      if (!by_launch) {
+        (void)hipEventRecord(w->done[w->gen & 1u], s);
+        w->prev_any = false;
+      }
+    }
   } mark{w, s};
   const bool direct = desc && (route == kRouteDirect ||
                                (route == kRouteAuto && a.n <= g_direct_max.load(std::memory_order_relaxed)));
@@ -464,7 +488,11 @@ int RunBatch(DeviceCtx& ctx, const SpanBatch& base_args, bool desc, bool verify,
     t_last_direct = true;
     t_last_stats = d.stats;
     t_last_stream = s;
-    hipError_t e = prismdb::dev::launch_direct(a, verify, ctx.cus, d, s);
+    mark.by_launch = true;
+    // PRISMDB_CRC32C_UNORDERED: every other call may overlap its predecessor
+    const bool any = unordered && !w->prev_any;
+    w->prev_any = any;
+    hipError_t e = prismdb::dev::launch_direct(a, verify, ctx.cus, d, s, w->done[w->gen & 1u], any);
     return e == hipSuccess ? 0 : FailHip(e, "direct kernel launch");
   }
   // The span kernel indexes records with 32 bits: cut larger batches.
@@ -586,7 +614,8 @@ int leveldb_crc32c_batch_fixed(const void* dev_base, size_t stride, size_t len, 
   if (nblocks == 0) return 0;
   if (dev_base == nullptr) return Fail(PRISMDB_CRC32C_EINVAL, "dev_base is NULL");
   if (len > 0xFFFFFFFFull) return Fail(PRISMDB_CRC32C_EINVAL, "len must be < 4 GiB");
-  if ((flags & ~(PRISMDB_CRC32C_MASK | PRISMDB_CRC32C_WRITE_TRAILER | PRISMDB_CRC32C_LOG_HEADER)) != 0)
+  if ((flags & ~(PRISMDB_CRC32C_MASK | PRISMDB_CRC32C_WRITE_TRAILER | PRISMDB_CRC32C_LOG_HEADER |
+                 PRISMDB_CRC32C_UNORDERED)) != 0)
     return Fail(PRISMDB_CRC32C_EINVAL, "unknown flag bits");
   if ((flags & PRISMDB_CRC32C_WRITE_TRAILER) && dev_mismatch != nullptr)
     return Fail(PRISMDB_CRC32C_EINVAL, "WRITE_TRAILER and verify are exclusive");
@@ -611,7 +640,8 @@ int leveldb_crc32c_batch(const void* dev_base, const uint64_t* dev_off, const ui
   if (n == 0) return 0;
   if (dev_base == nullptr || dev_off == nullptr || dev_len == nullptr)
     return Fail(PRISMDB_CRC32C_EINVAL, "dev_base/dev_off/dev_len must be non-NULL");
-  if ((flags & ~(PRISMDB_CRC32C_MASK | PRISMDB_CRC32C_WRITE_TRAILER | PRISMDB_CRC32C_LOG_HEADER)) != 0)
+  if ((flags & ~(PRISMDB_CRC32C_MASK | PRISMDB_CRC32C_WRITE_TRAILER | PRISMDB_CRC32C_LOG_HEADER |
+                 PRISMDB_CRC32C_UNORDERED)) != 0)
     return Fail(PRISMDB_CRC32C_EINVAL, "unknown flag bits");
   if ((flags & PRISMDB_CRC32C_WRITE_TRAILER) && dev_mismatch != nullptr)
     return Fail(PRISMDB_CRC32C_EINVAL, "WRITE_TRAILER and verify are exclusive");

@@ -147,13 +147,13 @@ struct SplitWs {
 constexpr uint64_t kDirectMaxSpans = 1ull << 17;
 constexpr int kDirectThreads = 768;  // per group, one group per CU: a wave's static run is <= 64 spans
                                      // while n <= 64 * 8 * CUs (host-checked)
-constexpr uint32_t kDirectTickets = 1u << 20;  // ticket workspace (beyond it: whole spans, one wave each)
+constexpr uint32_t kDirectTickets = 1u << 19;  // tickets per workspace slot (beyond: whole spans, one wave each)
 constexpr uint32_t kNullSpan = 0xFFFFFFFFu;
 
 struct DirectWs {
   unsigned long long* word;  // this call's supply << 32 | claimed: tickets pushed / tickets taken
-  unsigned long long* next;  // the next call's word (calls alternate; this call zeroes it)
-  uint32_t* tmap;            // per ticket: span, its first ticket, T | lg << 24, gen
+  unsigned long long* next;  // the word of the call after next (four words in turn; this call zeroes it)
+  uint32_t* tmap;            // per ticket, 32 B: span, first ticket, T | lg << 24, gen, off lo/hi, len, init
   uint32_t* part;            // per ticket: partial register
   uint32_t* cdone;           // per span, at its first ticket: tickets finished
   uint32_t* stats;           // cumulative: tickets adopted, spans folded whole, tickets claimed early / late
@@ -175,7 +175,13 @@ hipError_t launch_combine(const SpanBatch& a, bool desc, bool verify, const Spli
                           hipStream_t s);
 hipError_t launch_lane(const SpanBatch& a, bool verify, int grid, const SplitWs& ws, hipStream_t s);
 constexpr int kListThreads = 1024;  // crc32c_long_list_kernel block: one atomic per 16 runs
-hipError_t launch_direct(const SpanBatch& a, bool verify, int grid, const DirectWs& d, hipStream_t s);
+// `done` is recorded when the kernel completes (the launch's own completion
+// signal: a separate hipEventRecord marker cost ~5.7 us between back-to-back
+// calls).
+// any_order: the launch may start before the stream's previous kernel ends
+// (hipExtAnyOrderLaunch; PRISMDB_CRC32C_UNORDERED batches).
+hipError_t launch_direct(const SpanBatch& a, bool verify, int grid, const DirectWs& d, hipStream_t s,
+                         hipEvent_t done, bool any_order);
 hipError_t launch_scatter(const SpanBatch& a, const SplitWs& ws, const uint32_t* qout, const uint8_t* qmm,
                           hipStream_t s);
 

@@ -53,6 +53,8 @@
 // Test hooks (DirectWs::dbg): bit 0 delays every push by ~100 us, bit 1 makes
 // every worker claim once blindly (orphans); stats[] counts adopted tickets,
 // whole spans, worker claims and late claims.
+#include <hip/hip_ext.h>
+
 #include "crc32c_fold.h"
 
 namespace prismdb {
@@ -167,6 +169,16 @@ __global__ __launch_bounds__(kDirectThreads) void crc32c_direct_kernel(SpanBatch
     sbase = wave * q + (wave < r ? wave : r);
     m = q + (wave < r ? 1u : 0u);
   }
+  // A group works if any of its waves has a run or is a ticket worker
+  // (adopted tickets and whole spans belong to waves with a run); the others
+  // leave at once.  An active group's table words are requested first,
+  // before any wave of the chip has issued a data load: requested after the
+  // descriptors, they queued in HBM behind ~37 MB of other waves' first
+  // loads (~5 us, tools/direct_timeline.py).
+  const uint32_t g0 = blockIdx.x * kDirectWaves;
+  if (!(g0 < K || g0 + kDirectWaves > nwaves - workers)) return;
+  TableRegs<kDirectThreads> tr;
+  tables_issue(tr, a.tabs, tid);
   uint32_t voff_lo = 0, voff_hi = 0, vlen = 0, vinit = 0;
   if (lane < m) {
     const uint64_t off = a.off[sbase + lane];
@@ -210,11 +222,19 @@ __global__ __launch_bounds__(kDirectThreads) void crc32c_direct_kernel(SpanBatch
           const uint32_t src = (uint32_t)__builtin_ctzll(mm);
           mm &= mm - 1u;
           const uint32_t f0 = S0 + readlane(ex, src), Ts = readlane(T, src), lgs = readlane(lg, src);
+          // the span's descriptor rides in every entry: a claimer needs one
+          // read of its entry, not a second round trip to the descriptors
+          const uint32_t olo = readlane(voff_lo, src), ohi = readlane(voff_hi, src), ln = readlane(vlen, src),
+                         in = readlane(vinit, src);
           for (uint32_t k = lane; k < Ts; k += 64u) {
-            uint32_t* e = d.tmap + 4ull * (f0 + k);
+            uint32_t* e = d.tmap + 8ull * (f0 + k);
             e[0] = sbase + src;
             e[1] = f0;
             e[2] = Ts | (lgs << 24);
+            e[4] = olo;
+            e[5] = ohi;
+            e[6] = ln;
+            e[7] = in;
             __hip_atomic_store(e + 3, d.gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
           }
         }
@@ -230,7 +250,7 @@ __global__ __launch_bounds__(kDirectThreads) void crc32c_direct_kernel(SpanBatch
         if (lane == 0) atomicAdd(d.stats + 1, (uint32_t)__popcll(lm));
         const uint32_t hi = (uint64_t)S0 + total < d.cap ? S0 + total : d.cap;
         for (uint32_t k = S0 + lane; k < hi; k += 64u) {
-          uint32_t* e = d.tmap + 4ull * k;
+          uint32_t* e = d.tmap + 8ull * k;
           e[0] = kNullSpan;
           __hip_atomic_store(e + 3, d.gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         }
@@ -238,26 +258,13 @@ __global__ __launch_bounds__(kDirectThreads) void crc32c_direct_kernel(SpanBatch
     }
   }
 
-  // The next call's claim word starts at zero (calls on a stream alternate
-  // between the two; nothing in this call touches the other one).
+  // The claim word of the call after next starts at zero (calls take four
+  // words in turn, and at most two calls of a stream run at once).
   if (wave == 0 && lane == 0) __hip_atomic_store(d.next, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 
-  // A group without static work, adopted tickets, whole spans or workers
-  // leaves before loading the tables.  (The OR over the group goes through
-  // the table area: the tables take all of LDS.)  Idle waves do not look at
-  // `word`: thousands of reads of one address serialize in its L2 channel.
-  const bool work = m != 0u || adopt_lo < adopt_hi || worker;
-  const bool wwork = __ballot(work) != 0u;
-  if (lane == 0) lds[tid >> 6] = wwork ? 1u : 0u;
-  __syncthreads();
-  uint32_t any = 0;
-#pragma unroll
-  for (int k = 0; k < (int)kDirectWaves; ++k) any |= lds[k];
-  __syncthreads();
-  if (any != 0u) {
-    // ---- the static run's first loads go out before the table fill: the
-    // fill's own loads (one round trip) and its LDS writes then overlap the
-    // first data round trip instead of preceding it.
+  {
+    // ---- the static run's first loads go out before the table fill's LDS
+    // writes and barrier: those then overlap the first data round trip.
     const uint64_t inrun = m >= 64u ? ~0ull : (1ull << m) - 1ull;
     const uint64_t shortm = inrun & ~lm;
     // next short span of stream st at or after position j
@@ -284,7 +291,9 @@ __global__ __launch_bounds__(kDirectThreads) void crc32c_direct_kernel(SpanBatch
     // lane -- head bytes (lanes 0-2), tail bytes (3-5), stored crc (6-9).
     auto issue = [&](const DTask& t, uint32_t (&w)[kRounds], uint32_t& e) {
       const bool live = t.valid();
-      const uint32_t pad = t.pad(), h = t.h(), tl = t.t(), len = t.len();
+      // (readfirstlane: the load branches below must be scalar branches --
+      // as exec-masked branches, hipcc's CFG has paths that issue no loads)
+      const uint32_t pad = rfl(t.pad()), h = t.h(), tl = t.t(), len = t.len();
       const bool hwin = kVerify && hdr;
       auto sat = [](uint64_t x) -> uint32_t { return x > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)x; };
       const uint64_t start = t.body - h;
@@ -321,8 +330,6 @@ __global__ __launch_bounds__(kDirectThreads) void crc32c_direct_kernel(SpanBatch
 #pragma unroll
       for (int st = 0; st < 3; ++st) tk[sl][st] = static_task(jc[st], (uint32_t)st);  // (none without a run)
     }
-    TableRegs<kDirectThreads> tr;
-    tables_issue(tr, a.tabs, tid);
     // Every wave runs the ring (a wave without a run: empty tasks, whose
     // range-checked loads touch no memory, and no folds), so the ring's
     // registers have one definition on every path: hipCC then never copies
@@ -397,10 +404,10 @@ __global__ __launch_bounds__(kDirectThreads) void crc32c_direct_kernel(SpanBatch
           __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(t.body), (short)0, (int)t.z, 0x00020000);
       const uint32_t pad = t.pad(), h = t.h();
       r0 = 0u;
+      uint32_t hb = 0u;  // head bytes: requested before the chunk loads, used after them
       if (t.c == 0u) {
         const uint8_t* sp = reinterpret_cast<const uint8_t*>(t.body - h);
-        const uint32_t hb = lane < h ? (uint32_t)sp[lane] : 0u;
-        r0 = feed_short(ss, lane, init ^ kConditioning, edge_head(hb, h), h);
+        hb = lane < h ? (uint32_t)sp[lane] : 0u;
       }
       uint32_t acc = 0u;
       for (uint32_t c = t.c; c < t.c1; c += 2u) {
@@ -418,7 +425,10 @@ __global__ __launch_bounds__(kDirectThreads) void crc32c_direct_kernel(SpanBatch
           w0[j] = __builtin_amdgcn_raw_buffer_load_b32(rb, (int)o0, 0, 0);
           w1[j] = two ? __builtin_amdgcn_raw_buffer_load_b32(rb, (int)o1, 0, 0) : 0u;
         }
-        if (c == 0u && t.z != 0u) inject(w0, pad, r0);
+        if (c == 0u) {
+          r0 = feed_short(ss, lane, init ^ kConditioning, edge_head(hb, h), h);
+          if (t.z != 0u) inject(w0, pad, r0);
+        }
 #pragma unroll
         for (int j = 0; j < kRounds; ++j) acc = step256(lds, tab, acc, w0[j]);
         if (two) {
@@ -443,20 +453,26 @@ __global__ __launch_bounds__(kDirectThreads) void crc32c_direct_kernel(SpanBatch
     // Ticket tkt (< cap): spin until its map entry is this call's, fold its
     // chunks, store and count the partial; the span's last ticket combines
     // R = sum_k M^(T-1-k) R_k (M = shift_{4 KiB 2^lg}) and finishes the span.
+    // Every dependent memory round trip here costs microseconds while the
+    // static runs keep HBM saturated, so the path is cut to: entry (one
+    // 32-B read after its generation is seen), chunk loads, partial +
+    // counter, and for the span's last ticket one batch of loads (partials,
+    // combine columns, edge bytes) before the result.
     auto run_ticket = [&](uint32_t tkt) {
-      const uint32_t* e = d.tmap + 4ull * tkt;
+      const uint32_t* e = d.tmap + 8ull * tkt;
       while (rfl(load_acquire(e + 3)) != d.gen) __builtin_amdgcn_s_sleep(2);
-      const uint32_t sb = rfl(load_relaxed(e));
+      const uint32_t ew = lane < 8u ? load_relaxed(e + lane) : 0u;
+      const uint32_t sb = readlane(ew, 0);
       if (sb == kNullSpan) return;
-      const uint32_t f0 = rfl(load_relaxed(e + 1)), tn = rfl(load_relaxed(e + 2));
-      DTask t = geometry(base + const_load(a.off, sb), const_load(a.len, sb));
+      const uint32_t f0 = readlane(ew, 1), tn = readlane(ew, 2);
+      DTask t = geometry(base + (((uint64_t)readlane(ew, 5) << 32) | readlane(ew, 4)), readlane(ew, 6));
       t.b = sb;
       const uint32_t T = tn & 0xFFFFFFu, lg = tn >> 24, k = tkt - f0;
       const uint32_t first = t.c1 - ((T - 1u) << lg);  // ticket 0: the remainder
       t.c = k ? first + ((k - 1u) << lg) : 0u;
       t.c1 = k ? t.c + (1u << lg) : first;
       uint32_t r0 = 0;
-      const uint32_t v = group_reg(t, (k == 0u && has_init) ? const_load(a.init, sb) : 0u, r0);
+      const uint32_t v = group_reg(t, (k == 0u && has_init) ? readlane(ew, 7) : 0u, r0);
       uint32_t old = 0;
       if (lane == 0) {
         __hip_atomic_store(d.part + tkt, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -464,6 +480,11 @@ __global__ __launch_bounds__(kDirectThreads) void crc32c_direct_kernel(SpanBatch
       }
       if (readlane(old, 0) + 1u != T) return;
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      uint32_t tail = 0, stored = 0;
+      span_edges(t, tail, stored);
+      uint32_t cols[32];  // lane's final shift, requested with the partials
+#pragma unroll
+      for (int i = 0; i < 32; ++i) cols[i] = a.tabs->tick_lane[lg][i][lane];
       const uint32_t J = (T + 63u) >> 6;
       const int32_t pad0 = (int32_t)(J * 64u - T);
       uint32_t x = 0;
@@ -474,11 +495,9 @@ __global__ __launch_bounds__(kDirectThreads) void crc32c_direct_kernel(SpanBatch
       }
       uint32_t y = 0;
 #pragma unroll
-      for (int i = 0; i < 32; ++i) y ^= a.tabs->tick_lane[lg][i][lane] & (0u - ((x >> i) & 1u));
+      for (int i = 0; i < 32; ++i) y ^= cols[i] & (0u - ((x >> i) & 1u));
       const uint32_t R = wave_xor(y);
       if (lane == 0) __hip_atomic_store(d.cdone + f0, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      uint32_t tail = 0, stored = 0;
-      span_edges(t, tail, stored);
       finish(t, R, tail, stored, false);
     };
     // a long span of the run folded whole by this wave (ticket workspace full)
@@ -620,9 +639,13 @@ __global__ __launch_bounds__(kDirectThreads) void crc32c_direct_kernel(SpanBatch
 
 }
 
-hipError_t launch_direct(const SpanBatch& a, bool verify, int grid, const DirectWs& d, hipStream_t s) {
-  if (verify) crc32c_direct_kernel<true><<<grid, kDirectThreads, 0, s>>>(a, d);
-  else crc32c_direct_kernel<false><<<grid, kDirectThreads, 0, s>>>(a, d);
+hipError_t launch_direct(const SpanBatch& a, bool verify, int grid, const DirectWs& d, hipStream_t s,
+                         hipEvent_t done, bool any_order) {
+  const uint32_t fl = any_order ? (uint32_t)hipExtAnyOrderLaunch : 0u;
+  if (verify)
+    hipExtLaunchKernelGGL(crc32c_direct_kernel<true>, dim3(grid), dim3(kDirectThreads), 0, s, nullptr, done, fl, a, d);
+  else
+    hipExtLaunchKernelGGL(crc32c_direct_kernel<false>, dim3(grid), dim3(kDirectThreads), 0, s, nullptr, done, fl, a, d);
   return hipGetLastError();
 }
 

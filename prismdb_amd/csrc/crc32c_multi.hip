@@ -108,8 +108,10 @@ int leveldb_crc32c_batch_multi(int ndev, const int* devices, const void* const* 
     return MultiFail(PRISMDB_CRC32C_EINVAL, "batch_multi: devices/dev_base/dev_off/dev_len/n must be non-NULL");
   if (out0 == nullptr && mismatch0 == nullptr)
     return MultiFail(PRISMDB_CRC32C_EINVAL, "batch_multi: out0 or mismatch0 is needed");
-  if (flags & ~(PRISMDB_CRC32C_MASK | PRISMDB_CRC32C_WRITE_TRAILER | PRISMDB_CRC32C_LOG_HEADER))
+  if (flags & ~(PRISMDB_CRC32C_MASK | PRISMDB_CRC32C_WRITE_TRAILER | PRISMDB_CRC32C_LOG_HEADER |
+                PRISMDB_CRC32C_UNORDERED))
     return MultiFail(PRISMDB_CRC32C_EINVAL, "batch_multi: unknown flag bits");
+  flags &= ~PRISMDB_CRC32C_UNORDERED;  // (the clique's streams keep their calls in order)
   if ((flags & PRISMDB_CRC32C_WRITE_TRAILER) && mismatch0 != nullptr)
     return MultiFail(PRISMDB_CRC32C_EINVAL, "batch_multi: WRITE_TRAILER and verify are exclusive");
   for (int p = 0; p < ndev; ++p) {

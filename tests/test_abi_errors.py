@@ -46,7 +46,7 @@ def test_batch_rejects_null_descriptors(native, bufs):
     assert rc == EINVAL and "dev_base" in _err(native)
 
 
-@pytest.mark.parametrize("flags", [0x8, 0x100, 0xFFFFFFF0])
+@pytest.mark.parametrize("flags", [0x10, 0x100, 0xFFFFFFF0])
 def test_unknown_flag_bits(native, bufs, flags):
     data, off, ln, out, _ = bufs
     rc = native.leveldb_crc32c_batch(data.ctypes.data, off.ctypes.data, ln.ctypes.data, None, 4, out.ctypes.data,

@@ -295,12 +295,13 @@ def test_direct_concurrent_threads(dev, oracle):
 
 
 def test_thread_churn_device_memory_flat(dev, oracle, native):
-    """64 short-lived caller threads (8 at a time), each with its own stream,
-    one one-launch call and one planner call (two workspaces' worth of device
-    memory, > 50 MiB per thread): when a thread exits its workspaces go back
-    (stream-ordered frees behind the thread's last batch, pool trimmed), so
-    free device memory afterwards is where it was -- and the results are
-    right throughout."""
+    """64 short-lived caller threads (8 at a time), each with its own stream
+    and one file-sized call -- the first half on the one-launch path, the
+    second on the planner path (the route hook is set between waves, never
+    by the threads) -- each thread's workspaces (> 25 MiB of device memory)
+    go back when it exits (stream-ordered frees behind its last batch, pool
+    trimmed), so free device memory afterwards is where it was, and the
+    results are right throughout."""
     import torch
     from prismdb_amd import crc32c
 
@@ -314,13 +315,10 @@ def test_thread_churn_device_memory_flat(dev, oracle, native):
         try:
             s = torch.cuda.Stream()
             with torch.cuda.stream(s):
-                out = torch.empty((2, len(off)), dtype=torch.int32, device=dev)
-                crc32c.batch(buf, d_off, d_len, out=out[0], check_bounds=False, stream=s)  # one launch
-                prev = native.prismdb_crc32c_direct_max(0)  # (global hook: only this test's threads call)
-                crc32c.batch(buf, d_off, d_len, out=out[1], check_bounds=False, stream=s)  # planner
-                native.prismdb_crc32c_direct_max(prev)
+                out = torch.empty(len(off), dtype=torch.int32, device=dev)
+                crc32c.batch(buf, d_off, d_len, out=out, check_bounds=False, stream=s)
                 s.synchronize()
-                if not (out.cpu().numpy().view(np.uint32) == raw[None, :]).all():
+                if not (out.cpu().numpy().view(np.uint32) == raw).all():
                     errors.append(t)
         except Exception as e:  # noqa: BLE001 - reported below
             errors.append((t, repr(e)))
@@ -332,15 +330,67 @@ def test_thread_churn_device_memory_flat(dev, oracle, native):
         for x in th:
             x.join(120)
 
-    wave(0)  # torch's own per-thread state and the tensors above exist from here on
-    torch.cuda.synchronize()
-    torch.cuda.empty_cache()
-    free0, _ = torch.cuda.mem_get_info(dev)
-    for w in range(1, 8):
-        wave(8 * w)
+    prev = native.prismdb_crc32c_direct_max(1 << 17)
+    try:
+        wave(0)  # torch's own per-thread state and the tensors above exist from here on
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        free0, _ = torch.cuda.mem_get_info(dev)
+        for w in range(1, 8):
+            if w == 4:
+                native.prismdb_crc32c_direct_max(0)  # the planner path from here on
+            wave(8 * w)
+    finally:
+        native.prismdb_crc32c_direct_max(prev)
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
     free1, _ = torch.cuda.mem_get_info(dev)
     assert not errors, errors
-    # 56 leaked thread workspaces would be > 2.8 GiB
+    # 56 leaked thread workspaces would be > 1.4 GiB
     assert free0 - free1 < 256 << 20, (free0 - free1) / 2**20
+
+
+def test_unordered_file_calls(dev, oracle, native):
+    """PRISMDB_CRC32C_UNORDERED: 24 SST files sealed one call each, back to
+    back (every other launch may overlap its predecessor: the files are
+    disjoint), then all verified the same way (each file's verify after its
+    seal: at most the call just before may overlap), then an ordered verify
+    right after an unordered reseal of the same file.  Every result, every
+    trailer and every verify flag against the oracle."""
+    import torch
+    from prismdb_amd import crc32c
+
+    nf = 24
+    host, off, lens, raw, masked = _sst_file(oracle, 0x5EED00DB, files=nf)
+    sealed = host.copy()
+    tr = (off + lens.astype(np.uint64)).astype(np.int64)[:, None] + np.arange(4)[None, :]
+    host[tr] = 0  # trailers to be written
+    buf = torch.from_numpy(host).to(dev)
+    per = len(off) // nf
+    d_off = torch.from_numpy(off.astype(np.int64)).to(dev)
+    d_len = torch.from_numpy(lens.view(np.int32)).to(dev)
+    outs = torch.empty((3, len(off)), dtype=torch.int32, device=dev)
+    mms = torch.full((2, len(off)), 7, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+    for f in range(nf):
+        sl = slice(f * per, (f + 1) * per)
+        crc32c.batch(buf, d_off[sl], d_len[sl], mask=True, trailer=True, out=outs[0, sl], check_bounds=False,
+                     unordered=True)
+    for f in range(nf):
+        sl = slice(f * per, (f + 1) * per)
+        crc32c.batch(buf, d_off[sl], d_len[sl], verify=True, out=outs[1, sl], mismatch=mms[0, sl],
+                     check_bounds=False, unordered=True)
+    # ordered after unordered: file 0 resealed unordered, then verified in order
+    crc32c.batch(buf, d_off[:per], d_len[:per], mask=True, trailer=True, out=outs[2, :per], check_bounds=False,
+                 unordered=True)
+    crc32c.batch(buf, d_off[:per], d_len[:per], verify=True, out=outs[2, per:2 * per], mismatch=mms[1, :per],
+                 check_bounds=False)
+    torch.cuda.synchronize()
+    assert _last_split_rc(native) == -2  # the one-launch path
+    got = outs.cpu().numpy().view(np.uint32)
+    np.testing.assert_array_equal(got[0], masked)
+    np.testing.assert_array_equal(got[1], raw)
+    np.testing.assert_array_equal(got[2, :per], masked[:per])
+    np.testing.assert_array_equal(got[2, per:2 * per], raw[:per])
+    assert not mms.cpu().numpy()[0].any() and not mms.cpu().numpy()[1, :per].any()
+    assert (buf.cpu().numpy() == sealed).all()  # every trailer as the reference writes it

@@ -30,7 +30,11 @@ GIB = float(1 << 30)
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--only", nargs="*", help="workloads to run (default: all); e.g. wal_seal wal_verify")
     args = ap.parse_args()
+
+    def want(*names):
+        return not args.only or any(n in args.only for n in names)
     import numpy as np
     import torch
     from prismdb_amd import crc32c
@@ -64,57 +68,62 @@ def main():
     # config 3: mixed sizes
     rng = np.random.default_rng(0x5EED0003)
     lens = rng.choice([1024, 4096, 16384, 65536], size=(16 << 30) // 21760).astype(np.int64)
-    off = np.concatenate([[0], np.cumsum(lens)[:-1]])
-    d_off, d_len = torch.from_numpy(off).to(dev), torch.from_numpy(lens.astype(np.int32)).to(dev)
-    out = torch.empty(len(lens), dtype=torch.int32, device=dev)
-    t = timed(lambda: crc32c.batch(buf, d_off, d_len, out=out, check_bounds=False), args.reps)
-    report("config3_mixed", t, lens.sum(), lens.sum() + 16 * len(lens), len(lens))
-    del d_off, d_len, out
+    if want("config3_mixed"):
+        off = np.concatenate([[0], np.cumsum(lens)[:-1]])
+        d_off, d_len = torch.from_numpy(off).to(dev), torch.from_numpy(lens.astype(np.int32)).to(dev)
+        out = torch.empty(len(lens), dtype=torch.int32, device=dev)
+        t = timed(lambda: crc32c.batch(buf, d_off, d_len, out=out, check_bounds=False), args.reps)
+        report("config3_mixed", t, lens.sum(), lens.sum() + 16 * len(lens), len(lens))
+        del d_off, d_len, out
 
     # SST-shaped, fixed stride
     n = 1 << 24
-    out = torch.empty(n, dtype=torch.int32, device=dev)
-    t = timed(lambda: crc32c.batch_fixed(buf, 3992, 3988, n, out=out, mask=True), args.reps)
-    report("sst_fixed", t, n * 3988, n * (3988 + 4), n)
+    if want("sst_fixed"):
+        out = torch.empty(n, dtype=torch.int32, device=dev)
+        t = timed(lambda: crc32c.batch_fixed(buf, 3992, 3988, n, out=out, mask=True), args.reps)
+        report("sst_fixed", t, n * 3988, n * (3988 + 4), n)
 
     # SST-shaped, descriptors, with index spans (one per 64 MiB SST: 16 811 data spans)
-    per = 16811
-    files = n // (per + 122)
-    offs, lns = [], []
-    pos = 0
-    for _ in range(files):
-        offs.append(pos + np.arange(per, dtype=np.int64) * 3992)
-        lns.append(np.full(per, 3988, dtype=np.int64))
-        pos += per * 3992
-        offs.append(np.array([pos], dtype=np.int64))
-        lns.append(np.array([486977], dtype=np.int64))
-        pos += 486977 + 4 + 3
-        pos = (pos + 7) & ~7
-    off = np.concatenate(offs)
-    lens = np.concatenate(lns)
-    assert off[-1] + lens[-1] + 4 <= buf.numel()
-    d_off, d_len = torch.from_numpy(off).to(dev), torch.from_numpy(lens.astype(np.int32)).to(dev)
-    out2 = torch.empty(len(off), dtype=torch.int32, device=dev)
-    t = timed(lambda: crc32c.batch(buf, d_off, d_len, out=out2, mask=True, check_bounds=False), args.reps)
-    report("sst_desc", t, lens.sum(), lens.sum() + 16 * len(lens), len(lens))
-    del d_off, d_len, out2
+    if want("sst_desc"):
+        per = 16811
+        files = n // (per + 122)
+        offs, lns = [], []
+        pos = 0
+        for _ in range(files):
+            offs.append(pos + np.arange(per, dtype=np.int64) * 3992)
+            lns.append(np.full(per, 3988, dtype=np.int64))
+            pos += per * 3992
+            offs.append(np.array([pos], dtype=np.int64))
+            lns.append(np.array([486977], dtype=np.int64))
+            pos += 486977 + 4 + 3
+            pos = (pos + 7) & ~7
+        off = np.concatenate(offs)
+        lens = np.concatenate(lns)
+        assert off[-1] + lens[-1] + 4 <= buf.numel()
+        d_off, d_len = torch.from_numpy(off).to(dev), torch.from_numpy(lens.astype(np.int32)).to(dev)
+        out2 = torch.empty(len(off), dtype=torch.int32, device=dev)
+        t = timed(lambda: crc32c.batch(buf, d_off, d_len, out=out2, mask=True, check_bounds=False), args.reps)
+        report("sst_desc", t, lens.sum(), lens.sum() + 16 * len(lens), len(lens))
+        del d_off, d_len, out2
 
     # verify 4 KiB spans (fixed stride 4096, span 4092 B, trailer in the last 4 B)
-    out = torch.empty(n, dtype=torch.int32, device=dev)
-    mm = torch.empty(n, dtype=torch.uint8, device=dev)
-    t = timed(lambda: crc32c.batch_fixed(buf, 4096, 4092, n, out=out, mismatch=mm, verify=True), args.reps)
-    report("verify_4k", t, n * 4092, n * (4092 + 4 + 1 + 4), n)
+    if want("verify_4k"):
+        out = torch.empty(n, dtype=torch.int32, device=dev)
+        mm = torch.empty(n, dtype=torch.uint8, device=dev)
+        t = timed(lambda: crc32c.batch_fixed(buf, 4096, 4092, n, out=out, mismatch=mm, verify=True), args.reps)
+        report("verify_4k", t, n * 4092, n * (4092 + 4 + 1 + 4), n)
 
     # adversarial
     m = 2 << 20
-    lens = rng.integers(0, 70000, size=m).astype(np.int64)
-    off = np.sort(rng.integers(0, (16 << 30) - 70001, size=m)).astype(np.int64)
-    d_off, d_len = torch.from_numpy(off).to(dev), torch.from_numpy(lens.astype(np.int32)).to(dev)
-    out3 = torch.empty(m, dtype=torch.int32, device=dev)
-    t = timed(lambda: crc32c.batch(buf, d_off, d_len, out=out3, check_bounds=False), args.reps)
-    report("adversarial", t, lens.sum(), lens.sum() + 16 * m, m)
+    lens = rng.integers(0, 70000, size=m).astype(np.int64)  # (drawn either way: the WAL image below
+    off = np.sort(rng.integers(0, (16 << 30) - 70001, size=m)).astype(np.int64)  # comes from the same rng)
+    if want("adversarial"):
+        d_off, d_len = torch.from_numpy(off).to(dev), torch.from_numpy(lens.astype(np.int32)).to(dev)
+        out3 = torch.empty(m, dtype=torch.int32, device=dev)
+        t = timed(lambda: crc32c.batch(buf, d_off, d_len, out=out3, check_bounds=False), args.reps)
+        report("adversarial", t, lens.sum(), lens.sum() + 16 * m, m)
 
-    del d_off, d_len, out3
+        del d_off, d_len, out3
 
     # WAL: one 4 MiB log file of ~1 KB records written in log format, tiled
     from prismdb_amd import log

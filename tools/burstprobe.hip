@@ -74,6 +74,43 @@ __global__ __launch_bounds__(kThreads) void k_probe(const v4* __restrict__ buf, 
   (void)nthreads;
 }
 
+// The one-launch kernel's table fill (one round trip: 11 words + 3 x 16 B per
+// thread of a 36 KiB table, then 160 KiB of LDS writes), reading either one
+// shared table (every group the same addresses) or a private copy per group.
+template <bool kPrivate>
+__global__ __launch_bounds__(kThreads) void k_fill(const uint32_t* tab, uint32_t* out) {
+  __shared__ uint32_t lds[kLdsWords];
+  const uint32_t* t = tab + (kPrivate ? (size_t)blockIdx.x * 9216u : 0u);
+  uint32_t v[11];
+  v4 u[3];
+#pragma unroll
+  for (int i = 0; i < 11; ++i) {
+    const uint32_t x = threadIdx.x + (uint32_t)(i * kThreads);
+    const uint32_t q = x >> 3;
+    v[i] = x < 8192u ? t[(((q >> 9) << 1) | (q & 1u)) * 256u + ((q >> 1) & 255u)] : 0u;
+  }
+  const v4* nb = reinterpret_cast<const v4*>(t + 1024);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const uint32_t e = threadIdx.x + (uint32_t)(i * kThreads);
+    u[i] = e < 2048u ? nb[e] : v4{0, 0, 0, 0};
+  }
+  v4* dst = reinterpret_cast<v4*>(lds);
+#pragma unroll
+  for (int i = 0; i < 11; ++i) {
+    const uint32_t x = threadIdx.x + (uint32_t)(i * kThreads);
+    if (x < 8192u) dst[x] = v4{v[i], v[i], v[i], v[i]};
+  }
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const uint32_t e = threadIdx.x + (uint32_t)(i * kThreads);
+    if (e < 2048u) dst[8192u + e] = u[i];
+  }
+  __syncthreads();
+  const uint32_t acc = lds[(threadIdx.x * 41u) % kLdsWords];
+  if (acc == 0x12345678u) out[0] = acc;
+}
+
 int main(int argc, char** argv) {
   const size_t bytes = argc > 1 ? std::strtoull(argv[1], nullptr, 0) : 67529245ull;
   int dev = 0, cus = 0;
@@ -83,10 +120,10 @@ int main(int argc, char** argv) {
   v4* buf = nullptr;
   uint32_t *tab = nullptr, *out = nullptr;
   CHECK(hipMalloc(&buf, n16 * 16));
-  CHECK(hipMalloc(&tab, 9216 * 4));
+  CHECK(hipMalloc(&tab, (size_t)9216 * 4 * 1024));
   CHECK(hipMalloc(&out, 1 << 20));
   CHECK(hipMemset(buf, 0x5A, n16 * 16));
-  CHECK(hipMemset(tab, 0x11, 9216 * 4));
+  CHECK(hipMemset(tab, 0x11, (size_t)9216 * 4 * 1024));
   // grid: #CUs groups of 768 (the one-launch kernel's), or enough waves that
   // every lane's kPer loads cover the buffer, whichever is larger
   const size_t lanes = (n16 + kPer - 1) / kPer;
@@ -115,9 +152,22 @@ int main(int argc, char** argv) {
   const float t_lds = timed([&] { k_probe<true, false><<<cus, kThreads, 0, s>>>(buf, n16, tab, out); });
   const float t_read = timed([&] { k_probe<false, true><<<grid, kThreads, 0, s>>>(buf, n16, tab, out); });
   const float t_read_lds = timed([&] { k_probe<true, true><<<grid, kThreads, 0, s>>>(buf, n16, tab, out); });
+  // the fill right after a file-sized read (the table lines evicted from L2,
+  // as between back-to-back calls): read + fill pairs minus the reads alone
+  const float t_fill_shared = timed([&] {
+    k_probe<false, true><<<grid, kThreads, 0, s>>>(buf, n16, tab, out);
+    k_fill<false><<<cus, kThreads, 0, s>>>(tab, out);
+  }) - t_read;
+  const float t_fill_private = timed([&] {
+    k_probe<false, true><<<grid, kThreads, 0, s>>>(buf, n16, tab, out);
+    k_fill<true><<<cus, kThreads, 0, s>>>(tab, out);
+  }) - t_read;
+  const float t_fill_hot = timed([&] { k_fill<false><<<cus, kThreads, 0, s>>>(tab, out); });
   CHECK(hipGetLastError());
   std::printf("{\"bytes\": %zu, \"cus\": %d, \"grid_read\": %d, \"empty_us\": %.2f, \"lds_fill_us\": %.2f, "
-              "\"read_us\": %.2f, \"read_lds_us\": %.2f, \"read_TBps\": %.2f}\n",
-              bytes, cus, grid, t_empty, t_lds, t_read, t_read_lds, bytes / (t_read * 1e-6) / 1e12);
+              "\"read_us\": %.2f, \"read_lds_us\": %.2f, \"read_TBps\": %.2f, \"fill_hot_us\": %.2f, "
+              "\"fill_after_read_shared_us\": %.2f, \"fill_after_read_private_us\": %.2f}\n",
+              bytes, cus, grid, t_empty, t_lds, t_read, t_read_lds, bytes / (t_read * 1e-6) / 1e12, t_fill_hot,
+              t_fill_shared, t_fill_private);
   return 0;
 }

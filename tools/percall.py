@@ -11,7 +11,9 @@ one stream.
                     launch latency)
 
 for the one-launch path (the default for <= 2^17 spans) and, pinned by the
-test hook, the planner path; seal (MASK | WRITE_TRAILER), verify and plain.
+test hook, the planner path; seal (MASK | WRITE_TRAILER), verify and plain,
+and seal / verify with PRISMDB_CRC32C_UNORDERED alternating between two
+files (every other launch may overlap its predecessor).
 Prints one JSON object."""
 import json
 import os
@@ -35,6 +37,7 @@ def main():
     size = nd * 3992 + 486977 + 64
     buf = torch.empty(size, dtype=torch.uint8, device=dev)
     crc32c.fill_synthetic(buf, 0x5EED00F1)
+    buf2 = buf.clone()  # a second file: unordered calls alternate between the two
     off = np.concatenate([np.arange(nd, dtype=np.int64) * 3992, [nd * 3992]])
     lens = np.array([3988] * nd + [486977], dtype=np.int32)
     d_off = torch.from_numpy(off).to(dev)
@@ -42,6 +45,12 @@ def main():
     out = torch.empty(nd + 1, dtype=torch.int32, device=dev)
     mm = torch.empty(nd + 1, dtype=torch.uint8, device=dev)
     crc32c.batch(buf, d_off, d_len, mask=True, trailer=True)  # seal once: verify then passes
+    crc32c.batch(buf2, d_off, d_len, mask=True, trailer=True)
+    flip = [0]
+
+    def other():  # the file the previous unordered call did not touch
+        flip[0] ^= 1
+        return buf2 if flip[0] else buf
     s = torch.cuda.current_stream()
 
     def synced(fn, reps=200):
@@ -78,6 +87,11 @@ def main():
         "verify": lambda: crc32c.batch(buf, d_off, d_len, verify=True, out=out, mismatch=mm, check_bounds=False),
         "plain": lambda: crc32c.batch(buf, d_off, d_len, out=out, check_bounds=False),
         "data_only": lambda: crc32c.batch(buf, d_off[:nd], d_len[:nd], out=out[:nd], check_bounds=False),
+        # PRISMDB_CRC32C_UNORDERED: consecutive calls on two different files
+        "seal_unordered": lambda: crc32c.batch(other(), d_off, d_len, mask=True, trailer=True, out=out,
+                                               check_bounds=False, unordered=True),
+        "verify_unordered": lambda: crc32c.batch(other(), d_off, d_len, verify=True, out=out, mismatch=mm,
+                                                 check_bounds=False, unordered=True),
     }
     res = {"file": "16811 x 3988 B @ 3992 + 1 x 486977 B", "bytes": int(lens.astype(np.int64).sum())}
     native = lib()

@@ -47,7 +47,79 @@ VARIANTS = {
     "direct_nofold": [("crc32c_direct.hip",
                        "          for (int st = 0; st < 3; ++st) acc[st] = step256(lds, tab, acc[st], w[st][j]);",
                        "          for (int st = 0; st < 3; ++st) acc[st] ^= w[st][j];")] + MEASURE_ONLY,
+    # measurement-only (leaks workspaces at thread exit): no event recorded
+    # after each batch -- what the per-call hipEventRecord costs
+    "noevent": [("crc32c_capi.hip", "    ~MarkDone() { (void)hipEventRecord(w->done, s); }\n", "    ~MarkDone() {}\n")]
+    + MEASURE_ONLY,
+    # the one-launch kernel's completion marks the workspace event through
+    # hipExtLaunchKernel's stop event (no separate marker packet)
+    "extstop": [
+        ("crc32c_device.h",
+         "hipError_t launch_direct(const SpanBatch& a, bool verify, int grid, const DirectWs& d, hipStream_t s);",
+         "hipError_t launch_direct(const SpanBatch& a, bool verify, int grid, const DirectWs& d, hipStream_t s,\n"
+         "                         hipEvent_t done);"),
+        ("crc32c_direct.hip",
+         "hipError_t launch_direct(const SpanBatch& a, bool verify, int grid, const DirectWs& d, hipStream_t s) {\n"
+         "  if (verify) crc32c_direct_kernel<true><<<grid, kDirectThreads, 0, s>>>(a, d);\n"
+         "  else crc32c_direct_kernel<false><<<grid, kDirectThreads, 0, s>>>(a, d);\n",
+         "hipError_t launch_direct(const SpanBatch& a, bool verify, int grid, const DirectWs& d, hipStream_t s,\n"
+         "                         hipEvent_t done) {\n"
+         "  if (verify) hipExtLaunchKernelGGL(crc32c_direct_kernel<true>, dim3(grid), dim3(kDirectThreads), 0, s, nullptr, done, 0u, a, d);\n"
+         "  else hipExtLaunchKernelGGL(crc32c_direct_kernel<false>, dim3(grid), dim3(kDirectThreads), 0, s, nullptr, done, 0u, a, d);\n"),
+        ("crc32c_direct.hip", '#include "crc32c_fold.h"\n', '#include "crc32c_fold.h"\n#include <hip/hip_ext.h>\n'),
+        ("crc32c_capi.hip", "    ~MarkDone() { (void)hipEventRecord(w->done, s); }\n",
+         "    bool ext = false;\n    ~MarkDone() { if (!ext) (void)hipEventRecord(w->done, s); }\n"),
+        ("crc32c_capi.hip", "    hipError_t e = prismdb::dev::launch_direct(a, verify, ctx.cus, d, s);\n",
+         "    mark.ext = true;\n    hipError_t e = prismdb::dev::launch_direct(a, verify, ctx.cus, d, s, w->done);\n"),
+    ],
+    # the one-launch kernel's table words retired before slot 0 is issued
+    # (slot 0's loads then do not queue the table loads behind them)
+    "tables_first": [("crc32c_direct.hip",
+                      "#pragma unroll\n    for (int st = 0; st < 3; ++st) issue(tk[0][st], wb[0][st], eb[0][st]);\n"
+                      "    tables_wait<3 * (kRounds + 1)>(tr);  // slot 0's 51 loads stay in flight\n",
+                      "    tables_wait<0>(tr);\n"
+                      "#pragma unroll\n    for (int st = 0; st < 3; ++st) issue(tk[0][st], wb[0][st], eb[0][st]);\n")],
+    # tickets of one chunk (a 486 977-B index span: 119 tickets instead of 60)
+    "lg0": [("crc32c_direct.hip", "  return per <= 1u ? 0u : (per <= 2u ? 1u : (per <= 4u ? 2u : 3u));",
+             "  return 0u * per;")],
+    # twice the ticket workers (nwaves / 16)
+    "workers2x": [("crc32c_direct.hip", "  uint32_t reserve = nwaves / 32u;", "  uint32_t reserve = nwaves / 16u;")],
+    # measurement: per-wave phase timestamps (s_memrealtime, 100 MHz) written
+    # after the results: entry, descriptors in, tables in, first fold, ring
+    # drained, exit (tools/direct_timeline.py reads them)
+    "direct_ts": [
+        ("crc32c_direct.hip", "  const uint32_t nwaves = gridDim.x * kDirectWaves;\n",
+         "  const uint32_t nwaves = gridDim.x * kDirectWaves;\n"
+         "  const uint64_t ts0 = __builtin_amdgcn_s_memrealtime();\n  uint64_t ts1 = 0, ts2 = 0, ts3 = 0, ts4 = 0, tsw = 0;\n"),
+        ("crc32c_direct.hip", "    if (has_init) vinit = a.init[sbase + lane];\n  }\n",
+         "    if (has_init) vinit = a.init[sbase + lane];\n  }\n"
+         "  asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");\n  ts1 = __builtin_amdgcn_s_memrealtime();\n"),
+        ("crc32c_direct.hip", "    asm volatile(\"s_waitcnt lgkmcnt(0)\\n\\ts_barrier\" ::: \"memory\");\n",
+         "    asm volatile(\"s_waitcnt lgkmcnt(0)\\n\\ts_barrier\" ::: \"memory\");\n"
+         "    ts2 = __builtin_amdgcn_s_memrealtime();\n"),
+        ("crc32c_direct.hip",
+         "            if (tk[sl][0].valid() || tk[sl][1].valid() || tk[sl][2].valid()) fold(tk[sl], wb[sl], eb[sl]);\n",
+         "            if (tsw == 0) tsw = __builtin_amdgcn_s_memrealtime();\n"
+         "            if (tk[sl][0].valid() || tk[sl][1].valid() || tk[sl][2].valid()) fold(tk[sl], wb[sl], eb[sl]);\n"
+         "            if (ts3 == 0) ts3 = __builtin_amdgcn_s_memrealtime();\n"),
+        ("crc32c_direct.hip",
+         "          for (int st = 0; st < 3; ++st) wait_task<0>(wb[sl][st], eb[sl][st]);\n        }\n",
+         "          for (int st = 0; st < 3; ++st) wait_task<0>(wb[sl][st], eb[sl][st]);\n        }\n"
+         "        ts4 = __builtin_amdgcn_s_memrealtime();\n"),
+        ("crc32c_direct.hip", "    }\n  }\n\n}\n\nhipError_t launch_direct",
+         "    }\n  }\n  if (a.out != nullptr && lane < 8u) {\n"
+         "    const uint64_t ts5 = __builtin_amdgcn_s_memrealtime();\n"
+         "    uint64_t v = lane == 0 ? ts0 : lane == 1 ? ts1 : lane == 2 ? ts2 : lane == 3 ? ts3 : lane == 4 ? ts4 :\n"
+         "                 lane == 5 ? ts5 : lane == 6 ? (uint64_t)m : tsw;\n"
+         "    reinterpret_cast<uint64_t*>(a.out + ((n + 3u) & ~3u))[8u * wave + lane] = v;\n  }\n}\n\nhipError_t launch_direct"),
+    ] + MEASURE_ONLY,
 }
+
+# the previous commit's kernels (a git worktree under build/) with the stop-event launch
+VARIANTS["prev"] = [("@src", os.path.join(ROOT, "build", "wt_head", "prismdb_amd", "csrc"), None)] + VARIANTS["extstop"]
+# combinations
+VARIANTS["tf_ts"] = VARIANTS["tables_first"] + VARIANTS["direct_ts"]
+VARIANTS["tf_lg0_w2"] = VARIANTS["tables_first"] + VARIANTS["lg0"] + VARIANTS["workers2x"]
 
 
 def do_build(names):
@@ -60,11 +132,15 @@ def do_build(names):
         src = os.path.join(vroot, "pkg", "csrc")
         if os.path.isdir(src):
             shutil.rmtree(src)
-        shutil.copytree(CSRC, src)
+        spec = VARIANTS[name]
+        srcdir = CSRC
+        if spec and spec[0][0] == "@src":  # ("@src", directory, None): another checkout's sources
+            srcdir, spec = spec[0][1], spec[1:]
+        shutil.copytree(srcdir, src)
         inc = os.path.join(vroot, "include")
         if not os.path.exists(inc):
             os.symlink(os.path.join(ROOT, "include"), inc)
-        for fname, old, new in VARIANTS[name]:
+        for fname, old, new in spec:
             path = os.path.join(src, fname)
             with open(path) as f:
                 text = f.read()
