@@ -400,23 +400,24 @@ int PlannerWorkspace(Workspace& w, hipStream_t s, size_t nspans, uint32_t stream
 // The one-launch path's workspace: four claim words (call g uses word g % 4
 // and zeroes word (g + 2) % 4 for the call after next; at most two calls of a
 // stream are in flight, PRISMDB_CRC32C_UNORDERED), the usage counters, and
-// two slots (call parity) of: the ticket map (32-B entries carrying the
-// call's gen), the partial registers and the per-span ticket counters (zero
-// between calls: a span's combiner resets its own).
+// two slots (call parity) of: the ticket map (32-B entries of four words
+// tagged with the call's gen), the tagged partial registers and the per-span
+// ticket counters (zero between calls: a span's combiner resets its own).
 int DirectWorkspace(Workspace& w, hipStream_t s, prismdb::dev::DirectWs* out) {
   namespace d = prismdb::dev;
   const size_t cap = d::kDirectTickets;
-  const size_t slot_bytes = cap * (32 + 4 + 4);
+  const size_t slot_bytes = cap * (32 + 8 + 4);
   const size_t bytes = 256 + 2 * slot_bytes;
   if (w.direct == nullptr) {
     if (int rc = GrowBlock(&w.direct, bytes, s, "ticket workspace")) return rc;
     hipError_t e = hipMemsetAsync(w.direct, 0, bytes, s);
     if (e != hipSuccess) return FailHip(e, "ticket workspace memset");
   }
-  // Generations: map entries of earlier calls never match.  At the wrap
-  // (2^32 calls) the workspace is zeroed again (an ordered command: behind
-  // both slots' last calls) and the count restarts.
-  if (++w.gen == 0) {
+  // Generations: the words a call writes carry gen's low 16 bits (its tag),
+  // so words of earlier calls never match.  At the wrap (2^16 calls) the
+  // workspace is zeroed again (an ordered command: behind both slots' last
+  // calls) and the count restarts.
+  if ((++w.gen & d::kTagMask) == 0) {
     hipError_t e = hipMemsetAsync(w.direct, 0, bytes, s);
     if (e != hipSuccess) return FailHip(e, "ticket workspace memset");
     w.gen = 1;
@@ -427,12 +428,12 @@ int DirectWorkspace(Workspace& w, hipStream_t s, prismdb::dev::DirectWs* out) {
   out->next = reinterpret_cast<unsigned long long*>(p + 8 * ((w.gen + 2u) & 3u));
   out->stats = reinterpret_cast<uint32_t*>(p + 32);
   char* sl = p + 256 + (size_t)(w.gen & 1u) * slot_bytes;
-  out->tmap = reinterpret_cast<uint32_t*>(sl);
-  out->part = reinterpret_cast<uint32_t*>(sl + cap * 32);
-  out->cdone = reinterpret_cast<uint32_t*>(sl + cap * 36);
+  out->tmap = reinterpret_cast<uint64_t*>(sl);
+  out->part = reinterpret_cast<uint64_t*>(sl + cap * 32);
+  out->cdone = reinterpret_cast<uint32_t*>(sl + cap * 40);
   out->cap = g_direct_cap.load(std::memory_order_relaxed);
   out->dbg = g_direct_dbg.load(std::memory_order_relaxed);
-  out->gen = w.gen;  // 0 is the zeroed map's
+  out->tag = w.gen & d::kTagMask;  // 0 is the zeroed workspace's
   return 0;
 }
 

@@ -148,17 +148,24 @@ constexpr uint64_t kDirectMaxSpans = 1ull << 17;
 constexpr int kDirectThreads = 768;  // per group, one group per CU: a wave's static run is <= 64 spans
                                      // while n <= 64 * 8 * CUs (host-checked)
 constexpr uint32_t kDirectTickets = 1u << 19;  // tickets per workspace slot (beyond: whole spans, one wave each)
-constexpr uint32_t kNullSpan = 0xFFFFFFFFu;
+// Hand-offs between waves of the one-launch kernel carry the call's tag in
+// the top 16 bits of every 8-byte word (48-bit payload): a reader polls the
+// words it needs until each carries its call's tag.  Words are written and
+// read with relaxed agent-scope 8-B atomics (write-through / L2-served), so
+// no wave needs a release or acquire fence: those write back or invalidate
+// caches and wait for every load in flight (the table fill, the first data).
+constexpr uint32_t kTagShift = 48;
+constexpr uint32_t kTagMask = 0xFFFFu;
 
 struct DirectWs {
   unsigned long long* word;  // this call's supply << 32 | claimed: tickets pushed / tickets taken
   unsigned long long* next;  // the word of the call after next (four words in turn; this call zeroes it)
-  uint32_t* tmap;            // per ticket, 32 B: span, first ticket, T | lg << 24, gen, off lo/hi, len, init
-  uint32_t* part;            // per ticket: partial register
+  uint64_t* tmap;            // per ticket, 4 tagged words: span | (T-1, lg, k) << 32, span address, len, init
+  uint64_t* part;            // per ticket: tagged partial register
   uint32_t* cdone;           // per span, at its first ticket: tickets finished
   uint32_t* stats;           // cumulative: tickets adopted, spans folded whole, tickets claimed early / late
   uint32_t cap;              // tickets
-  uint32_t gen;              // this call's generation: tmap entries of earlier calls never match
+  uint32_t tag;              // this call's tag (1..0xFFFF): words of earlier calls never match
   uint32_t dbg;              // test hooks: bit 0 delays every push by ~100 us, bit 1 blind worker claims
 };
 

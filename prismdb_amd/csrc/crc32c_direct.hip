@@ -22,7 +22,8 @@
 //                g <= 8 that gives T <= 64; ticket 0 takes the remainder).  The
 //                wave pushes all its tickets with ONE 64-bit atomic on
 //                word = supply << 32 | claimed and writes the ticket map
-//                (span, first ticket, T | lg, gen -- gen last, release).
+//                (span | ticket index, span address, len, init: four 8-B
+//                words, each tagged with the call's tag, no fence).
 //   workers      the last nwaves / 32 waves have no run (at most 256 of them:
 //                every worker reads `word`, and same-address reads serialize
 //                in one L2 channel, ~2.5 ns each).  A worker polls `word` for
@@ -39,7 +40,11 @@
 // raced for the last visible ticket) belongs to whoever pushes ticket C: the
 // pusher sees claimed > its first ticket and folds those itself.  So no wave
 // waits for another wave's progress, except for a ticket-map entry that a
-// running wave is writing (its push came before the claim).  A ticket folds
+// running wave is writing (its push came before the claim) and a partial
+// whose store the counter add overtook.  Those hand-offs are tagged words
+// (kTagShift), polled: no release or acquire fence anywhere (a release
+// writes back the XCD's L2 and, like an acquire, waits for every load in
+// flight -- at the push, the table fill).  A ticket folds
 // its chunks into a partial register R_k (ticket 0 from the span's initial
 // register, the others from 0) with compiler-scheduled buffer loads; the wave
 // that finishes a span's last ticket (per-span counter) combines
@@ -69,12 +74,15 @@ __device__ __forceinline__ uint32_t ticket_lg(uint32_t nch) {
   return per <= 1u ? 0u : (per <= 2u ? 1u : (per <= 4u ? 2u : 3u));
 }
 
-__device__ __forceinline__ uint32_t load_relaxed(const uint32_t* p) {
+// Tagged 8-B words (kTagShift): relaxed agent-scope atomics, i.e. sc1
+// (write-through) stores and L2-served loads, no fences.
+__device__ __forceinline__ void put_tagged(uint64_t* p, uint32_t tag, uint64_t v) {
+  __hip_atomic_store(p, v | ((uint64_t)tag << kTagShift), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t get_word(const uint64_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ uint32_t load_acquire(const uint32_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-}
+__device__ __forceinline__ bool has_tag(uint64_t w, uint32_t tag) { return (uint32_t)(w >> kTagShift) == tag; }
 
 // Exclusive prefix sum of v over the wave; total = the sum.
 __device__ __forceinline__ uint32_t wave_excl_sum(uint32_t v, uint32_t lane, uint32_t& total) {
@@ -97,15 +105,19 @@ struct DTask {
   uint64_t body;  // first 4-B aligned byte of the span
   uint32_t z;     // body bytes (4 W)
   uint32_t f;     // pad | h << 10 | t << 12 | kind << 14 | result lane << 17 (static run)
+                  //   | ring chunk << 23 | ring chunks - 1 << 27 (static run: <= kRingChunks)
   uint32_t b;     // span
-  uint32_t c;     // first chunk
+  uint32_t c;     // first chunk (groups: tickets, whole spans)
   uint32_t c1;    // one past the last chunk
   __device__ uint32_t pad() const { return f & 1023u; }
   __device__ uint32_t h() const { return (f >> 10) & 3u; }
   __device__ uint32_t t() const { return (f >> 12) & 3u; }
   __device__ bool valid() const { return ((f >> 14) & 3u) != kKindNone; }
-  __device__ uint32_t slot() const { return f >> 17; }
+  __device__ uint32_t slot() const { return (f >> 17) & 63u; }
   __device__ uint32_t len() const { return h() + z + t(); }
+  // static run (the ring): the task's chunk, and whether it is the span's last
+  __device__ uint32_t rc() const { return (f >> 23) & 15u; }
+  __device__ bool rlast() const { return ((f >> 23) & 15u) == ((f >> 27) & 15u); }
 };
 
 // Span geometry: body, body bytes, pad | h << 10 | t << 12, chunks.
@@ -136,6 +148,18 @@ constexpr uint32_t kDirectWaves = kDirectThreads / 64u;
 // right after the static waves' discovery, mostly before the workers run.
 // A push the workers miss is claimed by its pusher after its run.
 constexpr uint64_t kWorkerPoll = 200u;
+// Spans of up to this many chunks (64 KiB) are folded by their run's wave in
+// the static ring, chunk after chunk on one stream; longer ones are cut into
+// tickets.  Tickets cost a claim on one shared word (same-address atomics
+// serialize in one L2 channel) and a chain of dependent round trips each: a
+// batch of 2^17 spans of 16-64 KiB as one-chunk tickets took 32 ms, as ring
+// tasks it streams.
+constexpr uint32_t kRingChunks = 16;
+static_assert(kRingChunks <= 16, "a ring task's chunk index and count take 4 bits each (DTask::f)");
+// A ticket-map entry's span field (24 bits: n <= kDirectMaxSpans) marking a
+// ticket nobody folds (the workspace was full: its span is folded whole).
+constexpr uint32_t kNullEntry = 0xFFFFFFu;
+static_assert(kDirectMaxSpans < kNullEntry, "span indices fit the entry's 24-bit field");
 
 template <bool kVerify>
 __global__ __launch_bounds__(kDirectThreads) void crc32c_direct_kernel(SpanBatch a, DirectWs d) {
@@ -188,14 +212,14 @@ __global__ __launch_bounds__(kDirectThreads) void crc32c_direct_kernel(SpanBatch
     if (has_init) vinit = a.init[sbase + lane];
   }
 
-  // ---- 1. discovery: the run's long spans (more than one chunk) -> tickets
+  // ---- 1. discovery: the run's long spans (more than kRingChunks chunks) -> tickets
   uint32_t adopt_lo = 0, adopt_hi = 0;  // orphans of this wave's push: its own to do
   uint64_t whole = 0;                   // workspace full: these run spans are folded whole here
   uint64_t lm = 0;                      // the run's long spans
   {
     const uint64_t p = base + (((uint64_t)voff_hi << 32) | voff_lo);
     const DTask g = geometry(p, vlen);
-    const bool lng = lane < m && g.c1 > 1u;
+    const bool lng = lane < m && g.c1 > kRingChunks;
     uint32_t T = 0, lg = 0;
     if (lng) {
       lg = ticket_lg(g.c1);
@@ -211,31 +235,29 @@ __global__ __launch_bounds__(kDirectThreads) void crc32c_direct_kernel(SpanBatch
       }
       uint64_t old = 0;
       if (lane == 0)
-        old = __hip_atomic_fetch_add(d.word, (unsigned long long)total << 32, __ATOMIC_ACQ_REL,
+        old = __hip_atomic_fetch_add(d.word, (unsigned long long)total << 32, __ATOMIC_RELAXED,
                                      __HIP_MEMORY_SCOPE_AGENT);
       const uint32_t S0 = readlane((uint32_t)(old >> 32), 0), C0 = readlane((uint32_t)old, 0);
       if ((uint64_t)S0 + total <= d.cap) {
-        // the ticket map, one long span at a time, 64 entries per step; the
-        // generation word is stored last (release), claimers spin on it
+        // the ticket map, one long span at a time, 64 entries per step: four
+        // tagged words each, in any order (a claimer polls until all four
+        // carry this call's tag; no fence, so the push does not wait for the
+        // table fill in flight).  The span's descriptor rides in every
+        // entry: a claimer needs one read of its entry, not a second round
+        // trip to the descriptors.
         uint64_t mm = lm;
         while (mm != 0u) {
           const uint32_t src = (uint32_t)__builtin_ctzll(mm);
           mm &= mm - 1u;
-          const uint32_t f0 = S0 + readlane(ex, src), Ts = readlane(T, src), lgs = readlane(lg, src);
-          // the span's descriptor rides in every entry: a claimer needs one
-          // read of its entry, not a second round trip to the descriptors
-          const uint32_t olo = readlane(voff_lo, src), ohi = readlane(voff_hi, src), ln = readlane(vlen, src),
-                         in = readlane(vinit, src);
+          const uint32_t f0 = S0 + readlane(ex, src), Ts = readlane(T, src);
+          const uint64_t addr = base + (((uint64_t)readlane(voff_hi, src) << 32) | readlane(voff_lo, src));
+          const uint32_t ln = readlane(vlen, src), in = readlane(vinit, src);
           for (uint32_t k = lane; k < Ts; k += 64u) {
-            uint32_t* e = d.tmap + 8ull * (f0 + k);
-            e[0] = sbase + src;
-            e[1] = f0;
-            e[2] = Ts | (lgs << 24);
-            e[4] = olo;
-            e[5] = ohi;
-            e[6] = ln;
-            e[7] = in;
-            __hip_atomic_store(e + 3, d.gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            uint64_t* e = d.tmap + 4ull * (f0 + k);
+            put_tagged(e + 0, d.tag, (uint64_t)(sbase + src) | ((uint64_t)k << 24));  // (T, lg: from len)
+            put_tagged(e + 1, d.tag, addr & ((1ull << kTagShift) - 1u));
+            put_tagged(e + 2, d.tag, ln);
+            put_tagged(e + 3, d.tag, in);
           }
         }
         if (C0 > S0) {
@@ -249,11 +271,7 @@ __global__ __launch_bounds__(kDirectThreads) void crc32c_direct_kernel(SpanBatch
         whole = lm;
         if (lane == 0) atomicAdd(d.stats + 1, (uint32_t)__popcll(lm));
         const uint32_t hi = (uint64_t)S0 + total < d.cap ? S0 + total : d.cap;
-        for (uint32_t k = S0 + lane; k < hi; k += 64u) {
-          uint32_t* e = d.tmap + 8ull * k;
-          e[0] = kNullSpan;
-          __hip_atomic_store(e + 3, d.gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        }
+        for (uint32_t k = S0 + lane; k < hi; k += 64u) put_tagged(d.tmap + 4ull * k, d.tag, kNullEntry);
       }
     }
   }
@@ -267,8 +285,15 @@ __global__ __launch_bounds__(kDirectThreads) void crc32c_direct_kernel(SpanBatch
     // writes and barrier: those then overlap the first data round trip.
     const uint64_t inrun = m >= 64u ? ~0ull : (1ull << m) - 1ull;
     const uint64_t shortm = inrun & ~lm;
-    // next short span of stream st at or after position j
-    auto static_task = [&](uint32_t& j, uint32_t st) -> DTask {
+    // Stream st's next task after `prev` (its last one): the next chunk of
+    // prev's span, or chunk 0 of the next ring span at or after position j
+    // (positions st mod 3).
+    auto static_task = [&](uint32_t& j, uint32_t st, const DTask& prev) -> DTask {
+      if (prev.valid() && !prev.rlast()) {
+        DTask t = prev;
+        t.f += 1u << 23;
+        return t;
+      }
       const uint64_t par = 0x9249249249249249ull << st;  // positions st mod 3
       const uint64_t from = j >= 64u ? 0ull : ~0ull << j;
       const uint64_t avail = shortm & par & from;
@@ -282,22 +307,31 @@ __global__ __launch_bounds__(kDirectThreads) void crc32c_direct_kernel(SpanBatch
       const uint64_t off = ((uint64_t)readlane(voff_hi, p) << 32) | readlane(voff_lo, p);
       DTask t = geometry(base + off, readlane(vlen, p));
       t.b = sbase + p;
-      t.f |= (kKindStatic << 14) | (p << 17);
+      t.f |= (kKindStatic << 14) | (p << 17) | ((t.c1 - 1u) << 27);  // (nch <= kRingChunks)
+      t.c = 0;  // (the ring reads the chunk from f)
+      t.c1 = 1;
       j = p + 3u;
       return t;
     };
-    // 17 loads per task, always: 16 body dwords (the buffer range check
-    // reads 0 outside the body: chunk 0's padding) and one edge byte per
-    // lane -- head bytes (lanes 0-2), tail bytes (3-5), stored crc (6-9).
+    // 17 loads per task, always: 16 body dwords of chunk t.c (the buffer
+    // range check reads 0 outside the body: chunk 0's padding) and one edge
+    // byte per lane -- head bytes (lanes 0-2, chunk 0), tail bytes (3-5) and
+    // stored crc (6-9) (the span's last chunk).
     auto issue = [&](const DTask& t, uint32_t (&w)[kRounds], uint32_t& e) {
       const bool live = t.valid();
       // (readfirstlane: the load branches below must be scalar branches --
       // as exec-masked branches, hipcc's CFG has paths that issue no loads)
-      const uint32_t pad = rfl(t.pad()), h = t.h(), tl = t.t(), len = t.len();
+      // chunk c > 0: the buffer starts at the chunk (no padding); chunk 0 is
+      // right-aligned, pad leading words read as 0 (no extra load branch:
+      // hipcc lowered one as an exec-masked branch around the ring's loads)
+      const uint32_t c = t.rc();
+      const bool first = c == 0u, last = t.rlast();
+      const uint32_t skip = first ? 0u : (c << 12) - 4u * t.pad();  // body bytes before chunk c
+      const uint32_t pad = rfl(first ? t.pad() : 0u), h = t.h(), tl = t.t(), len = t.len();
       const bool hwin = kVerify && hdr;
       auto sat = [](uint64_t x) -> uint32_t { return x > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)x; };
       const uint64_t start = t.body - h;
-      u32x4 rb = buffer_rsrc(reinterpret_cast<const uint8_t*>(t.body), live ? t.z : 0u);
+      u32x4 rb = buffer_rsrc(reinterpret_cast<const uint8_t*>(t.body + skip), live ? t.z - skip : 0u);
       u32x4 re = buffer_rsrc(reinterpret_cast<const uint8_t*>(hwin ? start - kLogCrcBack : start),
                              live ? (hwin ? sat((uint64_t)kLogCrcBack + len) : sat((uint64_t)len + (kVerify ? 4u : 0u)))
                                   : 0u);
@@ -316,9 +350,9 @@ __global__ __launch_bounds__(kDirectThreads) void crc32c_direct_kernel(SpanBatch
       }
       const uint32_t hb = hwin ? kLogCrcBack : 0u;  // edge-window offset of the span's first byte
       uint32_t eoff = 0xFFFFFFFFu;
-      if (lane < h) eoff = hb + lane;
-      if (lane >= 3u && lane < 3u + tl) eoff = sat((uint64_t)hb + h + t.z + (lane - 3u));
-      if (kVerify && lane >= 6u && lane < 10u) eoff = hwin ? lane - 6u : sat((uint64_t)len + (lane - 6u));
+      if (first && lane < h) eoff = hb + lane;
+      if (last && lane >= 3u && lane < 3u + tl) eoff = sat((uint64_t)hb + h + t.z + (lane - 3u));
+      if (kVerify && last && lane >= 6u && lane < 10u) eoff = hwin ? lane - 6u : sat((uint64_t)len + (lane - 6u));
       e = buf_ubyte(re, eoff);
     };
     DTask tk[2][3];
@@ -326,9 +360,11 @@ __global__ __launch_bounds__(kDirectThreads) void crc32c_direct_kernel(SpanBatch
     uint32_t eb[2][3];
     uint32_t jc[3] = {0u, 1u, 2u};
 #pragma unroll
-    for (int sl = 0; sl < 2; ++sl) {
-#pragma unroll
-      for (int st = 0; st < 3; ++st) tk[sl][st] = static_task(jc[st], (uint32_t)st);  // (none without a run)
+    for (int st = 0; st < 3; ++st) {
+      DTask none = geometry(base, 0u);
+      none.f = 0;
+      tk[0][st] = static_task(jc[st], (uint32_t)st, none);  // (none without a run)
+      tk[1][st] = static_task(jc[st], (uint32_t)st, tk[0][st]);
     }
     // Every wave runs the ring (a wave without a run: empty tasks, whose
     // range-checked loads touch no memory, and no folds), so the ring's
@@ -455,31 +491,42 @@ __global__ __launch_bounds__(kDirectThreads) void crc32c_direct_kernel(SpanBatch
     // R = sum_k M^(T-1-k) R_k (M = shift_{4 KiB 2^lg}) and finishes the span.
     // Every dependent memory round trip here costs microseconds while the
     // static runs keep HBM saturated, so the path is cut to: entry (one
-    // 32-B read after its generation is seen), chunk loads, partial +
+    // 32-B read, repeated until all four words carry the tag), chunk loads, partial +
     // counter, and for the span's last ticket one batch of loads (partials,
     // combine columns, edge bytes) before the result.
     auto run_ticket = [&](uint32_t tkt) {
-      const uint32_t* e = d.tmap + 8ull * tkt;
-      while (rfl(load_acquire(e + 3)) != d.gen) __builtin_amdgcn_s_sleep(2);
-      const uint32_t ew = lane < 8u ? load_relaxed(e + lane) : 0u;
-      const uint32_t sb = readlane(ew, 0);
-      if (sb == kNullSpan) return;
-      const uint32_t f0 = readlane(ew, 1), tn = readlane(ew, 2);
-      DTask t = geometry(base + (((uint64_t)readlane(ew, 5) << 32) | readlane(ew, 4)), readlane(ew, 6));
+      // lanes 0-3 read the entry's four words until every one carries this
+      // call's tag (a null entry: word 0 alone)
+      const uint64_t* e = d.tmap + 4ull * tkt;
+      uint64_t ew = 0;
+      for (;;) {
+        ew = lane < 4u ? get_word(e + lane) : 0u;
+        const uint64_t ok = __ballot(lane < 4u && has_tag(ew, d.tag));
+        if ((ok & 15u) == 15u || ((ok & 1u) && (readlane((uint32_t)ew, 0) & 0xFFFFFFu) == kNullEntry)) break;
+        __builtin_amdgcn_s_sleep(2);
+      }
+      const uint32_t w0lo = readlane((uint32_t)ew, 0), w0hi = readlane((uint32_t)(ew >> 32), 0);
+      const uint32_t sb = w0lo & 0xFFFFFFu;
+      if (sb == kNullEntry) return;
+      const uint32_t k = (w0lo >> 24) | ((w0hi & 0xFFFFu) << 8);
+      const uint64_t addr = ((uint64_t)(readlane((uint32_t)(ew >> 32), 1) & 0xFFFFu) << 32) | readlane((uint32_t)ew, 1);
+      DTask t = geometry(addr, readlane((uint32_t)ew, 2));
       t.b = sb;
-      const uint32_t T = tn & 0xFFFFFFu, lg = tn >> 24, k = tkt - f0;
+      const uint32_t lg = ticket_lg(t.c1), T = (t.c1 + (1u << lg) - 1u) >> lg, f0 = tkt - k;
       const uint32_t first = t.c1 - ((T - 1u) << lg);  // ticket 0: the remainder
       t.c = k ? first + ((k - 1u) << lg) : 0u;
       t.c1 = k ? t.c + (1u << lg) : first;
       uint32_t r0 = 0;
-      const uint32_t v = group_reg(t, (k == 0u && has_init) ? readlane(ew, 7) : 0u, r0);
+      const uint32_t v = group_reg(t, (k == 0u && has_init) ? readlane((uint32_t)ew, 3) : 0u, r0);
+      // the partial (tagged), then the span's counter: the wave whose add is
+      // the span's last combines, polling each partial until it carries the
+      // tag (the counter add may overtake another wave's partial store)
       uint32_t old = 0;
       if (lane == 0) {
-        __hip_atomic_store(d.part + tkt, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        old = __hip_atomic_fetch_add(d.cdone + f0, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        put_tagged(d.part + tkt, d.tag, v);
+        old = __hip_atomic_fetch_add(d.cdone + f0, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       if (readlane(old, 0) + 1u != T) return;
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       uint32_t tail = 0, stored = 0;
       span_edges(t, tail, stored);
       uint32_t cols[32];  // lane's final shift, requested with the partials
@@ -490,8 +537,13 @@ __global__ __launch_bounds__(kDirectThreads) void crc32c_direct_kernel(SpanBatch
       uint32_t x = 0;
       for (uint32_t j = 0; j < J; ++j) {
         const int32_t kk = (int32_t)(j * 64u + lane) - pad0;
-        const uint32_t s = kk >= 0 ? load_relaxed(d.part + f0 + (uint32_t)kk) : 0u;
-        x = gf2_apply(a.tabs->tick64[lg], x) ^ s;
+        uint64_t pw = 0;
+        for (;;) {
+          pw = kk >= 0 ? get_word(d.part + f0 + (uint32_t)kk) : ((uint64_t)d.tag << kTagShift);
+          if (__ballot(!has_tag(pw, d.tag)) == 0u) break;
+          __builtin_amdgcn_s_sleep(2);
+        }
+        x = gf2_apply(a.tabs->tick64[lg], x) ^ (uint32_t)pw;
       }
       uint32_t y = 0;
 #pragma unroll
@@ -514,7 +566,7 @@ __global__ __launch_bounds__(kDirectThreads) void crc32c_direct_kernel(SpanBatch
     auto claim = [&](uint32_t k, uint32_t& c, uint32_t& sp) {
       uint64_t old = 0;
       if (lane == 0)
-        old = __hip_atomic_fetch_add(d.word, (unsigned long long)k, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        old = __hip_atomic_fetch_add(d.word, (unsigned long long)k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       sp = readlane((uint32_t)(old >> 32), 0);
       c = readlane((uint32_t)old, 0);
     };
@@ -527,27 +579,34 @@ __global__ __launch_bounds__(kDirectThreads) void crc32c_direct_kernel(SpanBatch
     // With 12 waves per CU, an SST file's ~5.6 spans per wave are all
     // requested at once.
     {
+      // a stream's register between the chunks of its current span
+      uint32_t carry[3] = {0u, 0u, 0u};
       auto fold = [&](const DTask (&t)[3], uint32_t (&w)[3][kRounds], const uint32_t (&e)[3]) {
-        uint32_t r[3], acc[3] = {0u, 0u, 0u};
+        uint32_t r[3], acc[3];
 #pragma unroll
         for (int st = 0; st < 3; ++st) {
-          // initial register (init fed the head bytes) into body word 0
-          r[st] = feed_short(ss, lane, readlane(vinit, t[st].slot()) ^ kConditioning, edge_head(e[st], t[st].h()),
-                             t[st].h());
-          if (t[st].z) inject(w[st], t[st].pad(), r[st]);
+          r[st] = 0u;
+          acc[st] = carry[st];
+          if (t[st].rc() == 0u) {
+            // initial register (init fed the head bytes) into body word 0
+            r[st] = feed_short(ss, lane, readlane(vinit, t[st].slot()) ^ kConditioning, edge_head(e[st], t[st].h()),
+                               t[st].h());
+            acc[st] = 0u;
+            if (t[st].z) inject(w[st], t[st].pad(), r[st]);
+          }
         }
 #pragma unroll
         for (int j = 0; j < kRounds; ++j) {
 #pragma unroll
           for (int st = 0; st < 3; ++st) acc[st] = step256(lds, tab, acc[st], w[st][j]);
         }
-        uint32_t v[3];
-#pragma unroll
-        for (int st = 0; st < 3; ++st) v[st] = realign(lds, nibtab, acc[st]);
 #pragma unroll
         for (int st = 0; st < 3; ++st) {
-          const uint32_t bv = wave_xor(v[st]);
-          if (t[st].valid()) finish(t[st], t[st].z ? bv : r[st], edge_tail(e[st], t[st].t()), edge_stored(e[st]), true);
+          carry[st] = acc[st];
+          if (t[st].valid() && t[st].rlast()) {
+            const uint32_t bv = wave_xor(realign(lds, nibtab, acc[st]));
+            finish(t[st], t[st].z ? bv : r[st], edge_tail(e[st], t[st].t()), edge_stored(e[st]), true);
+          }
         }
       };
       {
@@ -564,7 +623,7 @@ __global__ __launch_bounds__(kDirectThreads) void crc32c_direct_kernel(SpanBatch
             if (tk[sl][0].valid() || tk[sl][1].valid() || tk[sl][2].valid()) fold(tk[sl], wb[sl], eb[sl]);
             if (!tk[sl ^ 1][0].valid() && !tk[sl ^ 1][1].valid() && !tk[sl ^ 1][2].valid()) goto drained;
 #pragma unroll
-            for (int st = 0; st < 3; ++st) tk[sl][st] = static_task(jc[st], (uint32_t)st);
+            for (int st = 0; st < 3; ++st) tk[sl][st] = static_task(jc[st], (uint32_t)st, tk[sl ^ 1][st]);
 #pragma unroll
             for (int st = 0; st < 3; ++st) issue(tk[sl][st], wb[sl][st], eb[sl][st]);
           }

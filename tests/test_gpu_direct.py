@@ -122,16 +122,21 @@ def test_sst_files_verify_damaged(dev, oracle, native, files):
     np.testing.assert_array_equal(_u32(out2), want2)
 
 
+RING_CHUNKS = 16  # kRingChunks: spans of up to 16 chunks of 4 KiB are folded in the static ring
+
+
 def test_tickets_claimed_and_combined(dev, oracle, native):
-    """Long spans of every ticket size (1, 2, 4 and 8 chunks per ticket, up to
-    128 tickets: a two-step combine) mixed with short ones, at odd offsets,
-    random init, MASK; the counters account for every ticket (claimed early,
-    late or adopted) and no span was folded whole."""
+    """Long spans (more than 16 chunks) of every ticket size (1, 2, 4 and 8
+    chunks per ticket, up to 128 tickets: a two-step combine) mixed with
+    short and ring-folded multi-chunk ones, at odd offsets, random init, MASK;
+    the counters account for every ticket (claimed early, late or adopted)
+    and no span was folded whole."""
     import torch
     from prismdb_amd import crc32c
 
     rng = np.random.default_rng(0x5EED00D3)
-    long_lens = [4097, 8192 + 5, 64 * 4096 + 1, 65 * 4096, 300_001, 1 << 20, (4 << 20) + 3, 2 * 4096 * 64 + 7]
+    long_lens = [4097, 8192 + 5, 16 * 4096 + 3, 20 * 4096 + 11, 64 * 4096 - 5, 64 * 4096 + 1, 65 * 4096, 300_001,
+                 1 << 20, (4 << 20) + 3, 2 * 4096 * 64 + 7]
     lens = np.concatenate([rng.integers(0, 4097, size=3000), long_lens]).astype(np.uint64)
     rng.shuffle(lens)
     gaps = rng.integers(0, 9, size=len(lens)).astype(np.uint64)
@@ -145,7 +150,7 @@ def test_tickets_claimed_and_combined(dev, oracle, native):
         h = min(h, L)
         W = (L - h) // 4
         nch = (W + 1023) // 1024
-        if nch <= 1:
+        if nch <= RING_CHUNKS:
             return 0
         per = (nch + 63) // 64
         lg = 0 if per <= 1 else 1 if per <= 2 else 2 if per <= 4 else 3
@@ -165,6 +170,97 @@ def test_tickets_claimed_and_combined(dev, oracle, native):
     d = after - before
     assert d[1] == 0  # no span folded whole
     assert d[0] + d[2] + d[3] == expect, (d, expect)
+
+
+@pytest.mark.parametrize("mode", ["plain", "verify", "seal", "log_verify"])
+def test_ring_multichunk_spans(dev, oracle, native, mode):
+    """Spans of 2..16 chunks are folded by their run's wave in the static
+    ring, chunk after chunk on one stream (no tickets: the counters do not
+    move).  Every chunk count at lengths around the chunk boundaries, every
+    start alignment, random init, mixed with one-chunk spans; verify against
+    a trailer (a few damaged), sealing (WRITE_TRAILER), and log-record verify
+    (the stored crc 6 B before the span)."""
+    import torch
+    from prismdb_amd import crc32c
+
+    rng = np.random.default_rng(0x5EED00E1 + len(mode))
+    lens = []
+    for k in range(1, RING_CHUNKS + 1):
+        for d in (-3, -1, 0, 1, 2, 5):
+            L = k * 4096 + d
+            if 0 < L <= RING_CHUNKS * 4096 - 4:  # body <= 16 chunks at any alignment
+                lens.append(L)
+    lens = np.array(lens + rng.integers(0, 4097, size=400).tolist() +
+                    rng.integers(4097, RING_CHUNKS * 4096 - 4, size=300).tolist(), dtype=np.uint64)
+    rng.shuffle(lens)
+    lead = 6 if mode == "log_verify" else 0
+    gaps = rng.integers(0, 8, size=len(lens)).astype(np.uint64) + 4 + lead
+    off = np.cumsum(np.concatenate([[5 + lead], (lens + gaps)[:-1]])).astype(np.uint64)
+    host = oracle.synth(int(off[-1] + lens[-1]) + 16, 0x5EED00E2)
+    n = len(lens)
+    init = rng.integers(0, 2**32, size=n, dtype=np.uint64).astype(np.uint32) if mode == "plain" else None
+    if mode in ("verify", "log_verify"):
+        raw, _ = oracle.batch(host, off, lens)
+        masked = np.array([oracle.mask(int(c)) for c in raw], dtype=np.uint32)
+        at = (off - 6) if mode == "log_verify" else (off + lens)
+        tr = at.astype(np.int64)[:, None] + np.arange(4)[None, :]
+        host[tr] = masked.astype("<u4").view(np.uint8).reshape(-1, 4)
+        for v in rng.choice(n, size=8, replace=False):  # damaged spans
+            host[int(off[v]) + int(lens[v]) // 2] ^= 0x40 if lens[v] else 0
+    buf = torch.from_numpy(host).to(dev)
+    d_off = torch.from_numpy(off.astype(np.int64)).to(dev)
+    d_len = torch.from_numpy(lens.astype(np.uint32).view(np.int32)).to(dev)
+    d_init = torch.from_numpy(init.view(np.int32)).to(dev) if init is not None else None
+    crc32c.batch(buf, d_off[:1], d_len[:1])
+    before = _stats(native)
+    if mode == "plain":
+        want, _ = oracle.batch(host, off, lens, init, mask=True)
+        out, _ = crc32c.batch(buf, d_off, d_len, d_init, mask=True)
+        np.testing.assert_array_equal(_u32(out), want)
+    elif mode == "seal":
+        raw, _ = oracle.batch(host, off, lens)
+        masked = np.array([oracle.mask(int(c)) for c in raw], dtype=np.uint32)
+        out, _ = crc32c.batch(buf, d_off, d_len, mask=True, trailer=True)
+        np.testing.assert_array_equal(_u32(out), masked)
+        got = buf.cpu().numpy()
+        tr = (off + lens).astype(np.int64)[:, None] + np.arange(4)[None, :]
+        np.testing.assert_array_equal(got[tr].reshape(-1).view("<u4"), masked)
+    else:
+        log = mode == "log_verify"
+        want, _ = oracle.batch(host, off, lens)
+        at = (off - 6) if log else (off + lens)
+        stored = host[at.astype(np.int64)[:, None] + np.arange(4)[None, :]].reshape(-1).view("<u4")
+        wmm = np.array([oracle.unmask(int(x)) != int(c) for x, c in zip(stored, want)], dtype=np.uint8)
+        out, mm = crc32c.batch(buf, d_off, d_len, verify=True, log_header=log)
+        np.testing.assert_array_equal(_u32(out), want)
+        np.testing.assert_array_equal(mm.cpu().numpy(), wmm)
+        assert 0 < int(wmm.sum()) <= 8
+    assert _last_split_rc(native) == -2  # the one-launch path
+    assert (_stats(native) - before).tolist() == [0, 0, 0, 0]  # no tickets, no whole spans
+
+
+def test_ring_batch_of_16_64k_spans(dev, oracle, native):
+    """A one-launch batch of 16 KiB and 64 KiB spans (LevelDB block_size
+    16/64 KiB; config 3's long sizes): all folded in the ring, no tickets
+    (as one-chunk tickets such batches took tens of ms).  4096 spans, all
+    checked."""
+    import torch
+    from prismdb_amd import crc32c
+
+    rng = np.random.default_rng(0x5EED00E3)
+    lens = rng.choice([16384, 65536, 16384 - 5, 65536 - 9], size=4096).astype(np.uint64)
+    off = np.concatenate([[0], np.cumsum(lens + 5)[:-1]]).astype(np.uint64) + 3
+    host = oracle.synth(int(off[-1] + lens[-1]) + 16, 0x5EED00E4)
+    want, _ = oracle.batch(host, off, lens)
+    buf = torch.from_numpy(host).to(dev)
+    d_off = torch.from_numpy(off.astype(np.int64)).to(dev)
+    d_len = torch.from_numpy(lens.astype(np.uint32).view(np.int32)).to(dev)
+    crc32c.batch(buf, d_off[:1], d_len[:1])
+    before = _stats(native)
+    out, _ = crc32c.batch(buf, d_off, d_len)
+    np.testing.assert_array_equal(_u32(out), want)
+    assert _last_split_rc(native) == -2
+    assert (_stats(native) - before).tolist() == [0, 0, 0, 0]
 
 
 def test_ticket_workspace_full_whole_spans(dev, oracle, native):

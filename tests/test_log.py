@@ -140,3 +140,46 @@ def test_seal_log_reproduces_writer_headers(native, log_cases):
                      torch.from_numpy(ln.astype(np.int32)).to(dev))
         torch.cuda.synchronize()
         assert (buf.cpu().numpy() == f).all(), name
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("with_out", [False, True])
+def test_seal_log_without_results(native, log_cases, with_out):
+    """The C ABI with out = NULL (and with it): every header crc resealed
+    byte-identical, log records of all lengths (the lane kernel's and the
+    generic path's) in one call; the lane kernel's results reach the header
+    stores through the workspace when the caller keeps none."""
+    import ctypes
+
+    import torch
+    from prismdb_amd import crc32c, log
+
+    dev = torch.device("cuda", 0)
+    cases = [(c, f) for c, f in log_cases if c["name"] in ("read_write", "many_blocks", "fragmentation",
+                                                             "marginal_trailer", "random_read")]
+    imgs, offs, lens, at = [], [], [], 0
+    for _, f in cases:
+        off, ln = log.scan(f)
+        imgs.append(f)
+        offs.append(off.astype(np.int64) + at + 6)  # type || payload
+        lens.append(ln.astype(np.int64) + 1)
+        at += len(f)
+    whole = np.concatenate(imgs)
+    g = whole.copy()
+    for o in np.concatenate(offs).tolist():
+        g[o - 6:o - 2] = 0
+    buf = torch.from_numpy(g).to(dev)
+    d_off = torch.from_numpy(np.concatenate(offs)).to(dev)
+    d_len = torch.from_numpy(np.concatenate(lens).astype(np.int32)).to(dev)
+    n = d_off.numel()
+    out = torch.empty(n, dtype=torch.int32, device=dev) if with_out else None
+    flags = crc32c.FLAG_MASK | crc32c.FLAG_WRITE_TRAILER | crc32c.FLAG_LOG_HEADER
+    rc = native.leveldb_crc32c_batch(buf.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), None, n,
+                                     out.data_ptr() if with_out else None, None, flags,
+                                     ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+    assert rc == 0
+    torch.cuda.synchronize()
+    assert (buf.cpu().numpy() == whole).all()
+    if with_out:
+        stored = whole[(np.concatenate(offs) - 6)[:, None] + np.arange(4)[None, :]].reshape(-1).view("<u4")
+        np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), stored)

@@ -15,6 +15,7 @@ test hook, the planner path; seal (MASK | WRITE_TRAILER), verify and plain,
 and seal / verify with PRISMDB_CRC32C_UNORDERED alternating between two
 files (every other launch may overlap its predecessor).
 Prints one JSON object."""
+import ctypes
 import json
 import os
 import statistics
@@ -102,6 +103,19 @@ def main():
             res[f"{route}_{name}_synced_us"] = synced(fn)
     native.prismdb_crc32c_direct_max(1 << 17)
     assert int(mm.sum().item()) == 0
+    # who folded the index span's tickets: per call, over 200 seal calls
+    # (stats: adopted orphans, spans folded whole, worker claims, late claims)
+    st = (ctypes.c_uint64 * 4)()
+    modes["seal"]()
+    torch.cuda.synchronize()
+    assert native.prismdb_crc32c_direct_stats(st) == 0
+    s0 = list(st)
+    for _ in range(200):
+        modes["seal"]()
+    torch.cuda.synchronize()
+    assert native.prismdb_crc32c_direct_stats(st) == 0
+    res["one_launch_tickets_per_call"] = dict(zip(("adopted", "whole", "worker", "late"),
+                                                  [round((b - a) / 200, 2) for a, b in zip(s0, st)]))
     res["fixed_data_blocks_back_to_back_us"] = b2b(lambda: crc32c.batch_fixed(buf, 3992, 3988, nd, out=out[:nd]))
     res["ideal_us_at_8TBps"] = round(res["bytes"] / 8e12 * 1e6, 2)
     res["ideal_us_at_6.5TBps"] = round(res["bytes"] / 6.5e12 * 1e6, 2)

@@ -84,6 +84,11 @@ VARIANTS = {
              "  return 0u * per;")],
     # twice the ticket workers (nwaves / 16)
     "workers2x": [("crc32c_direct.hip", "  uint32_t reserve = nwaves / 32u;", "  uint32_t reserve = nwaves / 16u;")],
+    # measurement-only (wrong results: no header written): the lane kernel
+    # sealing without its scattered header-crc stores -- what they cost
+    "lane_noseal": [("crc32c_kernels.hip",
+                     '          asm volatile("global_store_dword %0, %1, off" : : "v"(ta), "v"(v) : "memory");\n',
+                     '          (void)ta;\n')] + MEASURE_ONLY,
     # measurement: per-wave phase timestamps (s_memrealtime, 100 MHz) written
     # after the results: entry, descriptors in, tables in, first fold, ring
     # drained, exit (tools/direct_timeline.py reads them)
@@ -115,8 +120,9 @@ VARIANTS = {
     ] + MEASURE_ONLY,
 }
 
-# the previous commit's kernels (a git worktree under build/) with the stop-event launch
-VARIANTS["prev"] = [("@src", os.path.join(ROOT, "build", "wt_head", "prismdb_amd", "csrc"), None)] + VARIANTS["extstop"]
+# the previous commit's kernels (a git worktree under build/:
+# `git worktree add --detach build/wt_head HEAD`)
+VARIANTS["prev"] = [("@src", os.path.join(ROOT, "build", "wt_head", "prismdb_amd", "csrc"), None)]
 # combinations
 VARIANTS["tf_ts"] = VARIANTS["tables_first"] + VARIANTS["direct_ts"]
 VARIANTS["tf_lg0_w2"] = VARIANTS["tables_first"] + VARIANTS["lg0"] + VARIANTS["workers2x"]
