@@ -94,14 +94,14 @@ void BuildTables(DeviceTables* t) {
   // one-launch path: tickets of 2^lg chunks of 4 KiB
   const g::Op c = g::ShiftBytes(4096u);
   for (int i = 0; i < 32; ++i) t->shift_chunk[i] = c.col[i];
-  for (int lg = 0; lg < 4; ++lg) {
-    const uint64_t tb = 4096ull << lg;
-    const g::Op m64 = g::ShiftBytes(64ull * tb);
-    for (int i = 0; i < 32; ++i) t->tick64[lg][i] = m64.col[i];
-    for (int l = 0; l < 64; ++l) {
-      const g::Op m = g::ShiftBytes((63ull - (uint64_t)l) * tb);
-      for (int i = 0; i < 32; ++i) t->tick_lane[lg][i][l] = m.col[i];
+  for (int lg = 0; lg <= prismdb::dev::kTicketLgMax; ++lg) {
+    const g::Op m = g::ShiftBytes(4096ull << lg);
+    g::Op p = g::Identity();  // M^(63 - l), l = 63 down to 0; then M^64
+    for (int l = 63; l >= 0; --l) {
+      for (int i = 0; i < 32; ++i) t->tick_lane[lg][i][l] = p.col[i];
+      p = g::Compose(m, p);
     }
+    for (int i = 0; i < 32; ++i) t->tick64[lg][i] = p.col[i];
   }
 }
 
@@ -407,7 +407,7 @@ int DirectWorkspace(Workspace& w, hipStream_t s, prismdb::dev::DirectWs* out) {
   namespace d = prismdb::dev;
   const size_t cap = d::kDirectTickets;
   const size_t slot_bytes = cap * (32 + 8 + 4);
-  const size_t bytes = 256 + 2 * slot_bytes;
+  const size_t bytes = 256 + 4096 + 2 * slot_bytes;
   if (w.direct == nullptr) {
     if (int rc = GrowBlock(&w.direct, bytes, s, "ticket workspace")) return rc;
     hipError_t e = hipMemsetAsync(w.direct, 0, bytes, s);
@@ -427,7 +427,8 @@ int DirectWorkspace(Workspace& w, hipStream_t s, prismdb::dev::DirectWs* out) {
   out->word = reinterpret_cast<unsigned long long*>(p + 8 * (w.gen & 3u));
   out->next = reinterpret_cast<unsigned long long*>(p + 8 * ((w.gen + 2u) & 3u));
   out->stats = reinterpret_cast<uint32_t*>(p + 32);
-  char* sl = p + 256 + (size_t)(w.gen & 1u) * slot_bytes;
+  out->help = reinterpret_cast<uint32_t*>(p + 256);
+  char* sl = p + 256 + 4096 + (size_t)(w.gen & 1u) * slot_bytes;
   out->tmap = reinterpret_cast<uint64_t*>(sl);
   out->part = reinterpret_cast<uint64_t*>(sl + cap * 32);
   out->cdone = reinterpret_cast<uint32_t*>(sl + cap * 40);

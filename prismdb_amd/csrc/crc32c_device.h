@@ -35,6 +35,7 @@ constexpr uint32_t kLongSpan = 128u * 1024u;       // spans above this are split
 constexpr uint32_t kSegment = 32u * 1024u;         // ...into pieces of this size
 
 constexpr int kZeroWords = 16384;  // DeviceTables::zero: 256 regions of 256 B
+constexpr int kTicketLgMax = 14;   // one-launch tickets of up to 2^14 chunks (64 MiB)
 
 // Tables derived on the host from the polynomial (crc32c_gf2.h) and kept in HBM.
 struct DeviceTables {
@@ -45,9 +46,9 @@ struct DeviceTables {
   uint32_t lane_seg[32][64];  // [i][l] = column i of M^(63-l): lane l's final shift
   uint32_t slice4[4][256];    // slice4[k][b] = shift_4(b << 8k): one record per lane (lane kernel)
   // One-launch path (crc32c_direct.hip): a long span's tickets of g = 2^lg
-  // chunks (lg 0..3) are combined with M = shift_{4 KiB * g}:
-  uint32_t tick64[4][32];         // [lg][i] = column i of M^64
-  uint32_t tick_lane[4][32][64];  // [lg][i][l] = column i of M^(63-l): lane l's final shift
+  // chunks (lg 0..kTicketLgMax) are combined with M = shift_{4 KiB * g}:
+  uint32_t tick64[kTicketLgMax + 1][32];         // [lg][i] = column i of M^64
+  uint32_t tick_lane[kTicketLgMax + 1][32][64];  // [lg][i][l] = column i of M^(63-l): lane l's final shift
   uint32_t shift_chunk[32];       // column i of shift_{4 KiB} (tests; M for lg 0)
   // 64 KiB of zeros: the lane kernel's loads of lanes without a record to
   // read land here, 2 KiB per wave (wave % 32) -- one shared line was an L2
@@ -164,6 +165,7 @@ struct DirectWs {
   uint64_t* part;            // per ticket: tagged partial register
   uint32_t* cdone;           // per span, at its first ticket: tickets finished
   uint32_t* stats;           // cumulative: tickets adopted, spans folded whole, tickets claimed early / late
+  uint32_t* help;            // 32 replicas (128 B apart) of the help flag: == tag once a large push asks
   uint32_t cap;              // tickets
   uint32_t tag;              // this call's tag (1..0xFFFF): words of earlier calls never match
   uint32_t dbg;              // test hooks: bit 0 delays every push by ~100 us, bit 1 blind worker claims

@@ -67,12 +67,17 @@ namespace dev {
 
 namespace {
 
-// Chunks per ticket: 2^lg, the smallest power of two <= 8 that keeps a span
-// at <= 64 tickets (one Horner step in the combine).
+// Chunks per ticket: 2^lg, the smallest power of two that keeps a span at
+// <= 64 tickets (one Horner step in the combine; any span of < 4 GiB), and
+// at least 2^kTicketLgMin.  Tickets were <= 8 chunks: a 64 MiB span was
+// 2048 tickets, and 127 such spans took 26 ms through 96 ticket workers.
+constexpr uint32_t kTicketLgMin = 2;
 __device__ __forceinline__ uint32_t ticket_lg(uint32_t nch) {
-  const uint32_t per = (nch + 63u) >> 6;  // ceil(nch / 64)
-  return per <= 1u ? 0u : (per <= 2u ? 1u : (per <= 4u ? 2u : 3u));
+  const uint32_t per = (nch + 63u) >> 6;  // ceil(nch / 64) >= 1
+  const uint32_t lg = per <= 1u ? 0u : 32u - (uint32_t)__builtin_clz(per - 1u);  // ceil(log2(per))
+  return lg < kTicketLgMin ? kTicketLgMin : lg;
 }
+static_assert(kTicketLgMax >= 14, "2^20 chunks (4 GiB) in 64 tickets");
 
 // Tagged 8-B words (kTagShift): relaxed agent-scope atomics, i.e. sc1
 // (write-through) stores and L2-served loads, no fences.
@@ -104,8 +109,8 @@ enum : uint32_t { kKindNone = 0, kKindStatic = 1 };
 struct DTask {
   uint64_t body;  // first 4-B aligned byte of the span
   uint32_t z;     // body bytes (4 W)
-  uint32_t f;     // pad | h << 10 | t << 12 | kind << 14 | result lane << 17 (static run)
-                  //   | ring chunk << 23 | ring chunks - 1 << 27 (static run: <= kRingChunks)
+  uint32_t f;     // pad | h << 10 | t << 12 | kind << 14 | result lane << 16 (static run)
+                  //   | ring chunk << 22 | ring chunks - 1 << 27 (static run: <= kRingChunks)
   uint32_t b;     // span
   uint32_t c;     // first chunk (groups: tickets, whole spans)
   uint32_t c1;    // one past the last chunk
@@ -113,11 +118,11 @@ struct DTask {
   __device__ uint32_t h() const { return (f >> 10) & 3u; }
   __device__ uint32_t t() const { return (f >> 12) & 3u; }
   __device__ bool valid() const { return ((f >> 14) & 3u) != kKindNone; }
-  __device__ uint32_t slot() const { return (f >> 17) & 63u; }
+  __device__ uint32_t slot() const { return (f >> 16) & 63u; }
   __device__ uint32_t len() const { return h() + z + t(); }
   // static run (the ring): the task's chunk, and whether it is the span's last
-  __device__ uint32_t rc() const { return (f >> 23) & 15u; }
-  __device__ bool rlast() const { return ((f >> 23) & 15u) == ((f >> 27) & 15u); }
+  __device__ uint32_t rc() const { return (f >> 22) & 31u; }
+  __device__ bool rlast() const { return ((f >> 22) & 31u) == (f >> 27); }
 };
 
 // Span geometry: body, body bytes, pad | h << 10 | t << 12, chunks.
@@ -148,17 +153,26 @@ constexpr uint32_t kDirectWaves = kDirectThreads / 64u;
 // right after the static waves' discovery, mostly before the workers run.
 // A push the workers miss is claimed by its pusher after its run.
 constexpr uint64_t kWorkerPoll = 200u;
-// Spans of up to this many chunks (64 KiB) are folded by their run's wave in
+// Spans of up to this many chunks (128 KiB) are folded by their run's wave in
 // the static ring, chunk after chunk on one stream; longer ones are cut into
 // tickets.  Tickets cost a claim on one shared word (same-address atomics
 // serialize in one L2 channel) and a chain of dependent round trips each: a
-// batch of 2^17 spans of 16-64 KiB as one-chunk tickets took 32 ms, as ring
-// tasks it streams.
-constexpr uint32_t kRingChunks = 16;
-static_assert(kRingChunks <= 16, "a ring task's chunk index and count take 4 bits each (DTask::f)");
+// batch of 2^17 spans of 16-64 KiB as one-chunk tickets took 222 ms, as ring
+// tasks 4.3 ms; 122 K spans of 0-70 000 B took 4.6 ms with 17-chunk spans
+// as tickets.
+constexpr uint32_t kRingChunks = 32;
+static_assert(kRingChunks <= 32, "a ring task's chunk index and count take 5 bits each (DTask::f)");
 // A ticket-map entry's span field (24 bits: n <= kDirectMaxSpans) marking a
 // ticket nobody folds (the workspace was full: its span is folded whole).
 constexpr uint32_t kNullEntry = 0xFFFFFFu;
+// A push of at least this many chunks of ticket work (1 MiB) calls every
+// static wave to claim tickets after its run (an SST file's index block,
+// 119 chunks, stays with the ticket workers).
+constexpr uint32_t kHelpChunks = 256;
+// How long a wave of an idle group waits for the help flag (s_memrealtime
+// ticks, 100 MHz): 3 us.  Pushes come right after the static waves' first
+// descriptor loads (~1.5-2.5 us into the kernel).
+constexpr uint64_t kHelpPoll = 300u;
 static_assert(kDirectMaxSpans < kNullEntry, "span indices fit the entry's 24-bit field");
 
 template <bool kVerify>
@@ -194,13 +208,36 @@ __global__ __launch_bounds__(kDirectThreads) void crc32c_direct_kernel(SpanBatch
     m = q + (wave < r ? 1u : 0u);
   }
   // A group works if any of its waves has a run or is a ticket worker
-  // (adopted tickets and whole spans belong to waves with a run); the others
-  // leave at once.  An active group's table words are requested first,
+  // (adopted tickets and whole spans belong to waves with a run).  The
+  // others (batches of fewer spans than waves) wait up to kHelpPoll for a
+  // large push's help flag (its replica for this group; one lane polls, the
+  // group meets at a barrier) and leave unless it comes: with a few huge
+  // spans, 127 static waves and 256 ticket workers folded 8 GiB of tickets
+  // at 1.4 TB/s.  An active group's table words are requested first,
   // before any wave of the chip has issued a data load: requested after the
   // descriptors, they queued in HBM behind ~37 MB of other waves' first
   // loads (~5 us, tools/direct_timeline.py).
   const uint32_t g0 = blockIdx.x * kDirectWaves;
-  if (!(g0 < K || g0 + kDirectWaves > nwaves - workers)) return;
+  bool helper = false;  // a wave of an idle group called in by the help flag
+  if (!(g0 < K || g0 + kDirectWaves > nwaves - workers)) {
+    if (tid == 0) {
+      uint32_t go = 0;
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      for (;;) {
+        if (__hip_atomic_load(d.help + 32u * (blockIdx.x & 31u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == d.tag) {
+          go = 1;
+          break;
+        }
+        if (__builtin_amdgcn_s_memrealtime() - t0 > kHelpPoll) break;
+        __builtin_amdgcn_s_sleep(16);
+      }
+      lds[0] = go;
+    }
+    __syncthreads();
+    if (lds[0] == 0u) return;
+    __syncthreads();  // (the table fill overwrites lds[0])
+    helper = true;
+  }
   TableRegs<kDirectThreads> tr;
   tables_issue(tr, a.tabs, tid);
   uint32_t voff_lo = 0, voff_hi = 0, vlen = 0, vinit = 0;
@@ -227,8 +264,9 @@ __global__ __launch_bounds__(kDirectThreads) void crc32c_direct_kernel(SpanBatch
     }
     lm = __ballot(lng);
     if (lm != 0u) {
-      uint32_t total = 0;
+      uint32_t total = 0, chunks = 0;
       const uint32_t ex = wave_excl_sum(T, lane, total);
+      (void)wave_excl_sum(lng ? g.c1 : 0u, lane, chunks);
       if (d.dbg & 1u) {  // test hook: push late, after other waves have run out of claims
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         while (__builtin_amdgcn_s_memrealtime() - t0 < 10000u) __builtin_amdgcn_s_sleep(64);
@@ -260,6 +298,11 @@ __global__ __launch_bounds__(kDirectThreads) void crc32c_direct_kernel(SpanBatch
             put_tagged(e + 3, d.tag, in);
           }
         }
+        // A large push (>= kHelpChunks of ticket work) calls every wave to
+        // claim after its run: the 96-256 ticket workers alone took 26 ms
+        // over 127 spans of 64 MiB.
+        if (chunks >= kHelpChunks && lane < 32u)
+          __hip_atomic_store(d.help + 32u * lane, d.tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (C0 > S0) {
           adopt_lo = S0;
           adopt_hi = C0 < S0 + total ? C0 : S0 + total;
@@ -291,7 +334,7 @@ __global__ __launch_bounds__(kDirectThreads) void crc32c_direct_kernel(SpanBatch
     auto static_task = [&](uint32_t& j, uint32_t st, const DTask& prev) -> DTask {
       if (prev.valid() && !prev.rlast()) {
         DTask t = prev;
-        t.f += 1u << 23;
+        t.f += 1u << 22;
         return t;
       }
       const uint64_t par = 0x9249249249249249ull << st;  // positions st mod 3
@@ -307,7 +350,7 @@ __global__ __launch_bounds__(kDirectThreads) void crc32c_direct_kernel(SpanBatch
       const uint64_t off = ((uint64_t)readlane(voff_hi, p) << 32) | readlane(voff_lo, p);
       DTask t = geometry(base + off, readlane(vlen, p));
       t.b = sbase + p;
-      t.f |= (kKindStatic << 14) | (p << 17) | ((t.c1 - 1u) << 27);  // (nch <= kRingChunks)
+      t.f |= (kKindStatic << 14) | (p << 16) | ((t.c1 - 1u) << 27);  // (nch <= kRingChunks)
       t.c = 0;  // (the ring reads the chunk from f)
       t.c1 = 1;
       j = p + 3u;
@@ -446,9 +489,13 @@ __global__ __launch_bounds__(kDirectThreads) void crc32c_direct_kernel(SpanBatch
         hb = lane < h ? (uint32_t)sp[lane] : 0u;
       }
       uint32_t acc = 0u;
-      for (uint32_t c = t.c; c < t.c1; c += 2u) {
-        const bool two = c + 1u < t.c1;
-        uint32_t w0[kRounds], w1[kRounds];
+      // Two chunks (32 loads, 8 KiB) per step, the next step's loads issued
+      // before this step's fold: two steps in flight (a 1 MiB ticket is 128
+      // steps; four-chunk steps spilled VGPRs to scratch).  Chunks past t.c1
+      // read as 0 (a zero count) and are not folded.
+      constexpr int kG = 2;
+      auto load_step = [&](uint32_t c, uint32_t (&w)[kG][kRounds]) {
+        const uint32_t nin = c >= t.c1 ? 0u : (t.c1 - c < (uint32_t)kG ? t.c1 - c : (uint32_t)kG);
         const uint32_t i0 = (c << 10) + lane - pad;  // chunk 0: wraps below the body
 #pragma unroll
         for (int j = 0; j < kRounds; ++j) {
@@ -456,21 +503,39 @@ __global__ __launch_bounds__(kDirectThreads) void crc32c_direct_kernel(SpanBatch
           // immediate offset, a wrapped (negative) voffset + imm is a sum past
           // 2^32, which the range check reads as out of range -- zeros where
           // chunk 0's body words are (the span kernel's note on chunk 0).
-          uint32_t o0 = (i0 + 64u * (uint32_t)j) * 4u, o1 = o0 + 4096u;
-          asm volatile("" : "+v"(o0), "+v"(o1));
-          w0[j] = __builtin_amdgcn_raw_buffer_load_b32(rb, (int)o0, 0, 0);
-          w1[j] = two ? __builtin_amdgcn_raw_buffer_load_b32(rb, (int)o1, 0, 0) : 0u;
+          uint32_t o0 = (i0 + 64u * (uint32_t)j) * 4u;
+          asm volatile("" : "+v"(o0));
+#pragma unroll
+          for (int k = 0; k < kG; ++k)
+            w[k][j] = (uint32_t)k < nin ? __builtin_amdgcn_raw_buffer_load_b32(rb, (int)(o0 + 4096u * k), 0, 0) : 0u;
         }
+      };
+      auto fold_step = [&](uint32_t c, uint32_t (&w)[kG][kRounds]) {
+        const uint32_t nin = t.c1 - c < (uint32_t)kG ? t.c1 - c : (uint32_t)kG;
         if (c == 0u) {
           r0 = feed_short(ss, lane, init ^ kConditioning, edge_head(hb, h), h);
-          if (t.z != 0u) inject(w0, pad, r0);
+          if (t.z != 0u) inject(w[0], pad, r0);
         }
 #pragma unroll
-        for (int j = 0; j < kRounds; ++j) acc = step256(lds, tab, acc, w0[j]);
-        if (two) {
+        for (int k = 0; k < kG; ++k) {
+          if ((uint32_t)k < nin) {
 #pragma unroll
-          for (int j = 0; j < kRounds; ++j) acc = step256(lds, tab, acc, w1[j]);
+            for (int j = 0; j < kRounds; ++j) acc = step256(lds, tab, acc, w[k][j]);
+          }
         }
+      };
+      uint32_t wa[kG][kRounds], wb2[kG][kRounds];
+      uint32_t c = t.c;
+      load_step(c, wa);
+      for (;;) {
+        load_step(c + kG, wb2);
+        fold_step(c, wa);
+        c += kG;
+        if (c >= t.c1) break;
+        load_step(c + kG, wa);
+        fold_step(c, wb2);
+        c += kG;
+        if (c >= t.c1) break;
       }
       return wave_xor(realign(lds, nibtab, acc));
     };
@@ -676,9 +741,14 @@ __global__ __launch_bounds__(kDirectThreads) void crc32c_direct_kernel(SpanBatch
     // ---- late: a wave that pushed tickets claims, one at a time, until
     // none is left -- its own included, whoever else did not take them, so
     // every pushed ticket is claimed by someone (a claim past the supply is an
-    // orphan: its pusher does it).  Other static waves leave: 3072 reads of
+    // orphan: its pusher does it).  Other static waves join only when a large
+    // push called for help (one read of their replica of the help flag, 32
+    // replicas on lines of their own); otherwise they leave: 3072 reads of
     // `word` at the end cost ~8 us of the kernel's tail.
-    while (lm != 0u && whole == 0u) {
+    bool help = helper;
+    if (lm == 0u && wave < K)
+      help = __hip_atomic_load(d.help + 32u * (wave & 31u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == d.tag;
+    while ((lm != 0u || help) && whole == 0u) {
       uint64_t wd = 0;
       if (lane == 0) wd = __hip_atomic_load(d.word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (readlane((uint32_t)(wd >> 32), 0) <= readlane((uint32_t)wd, 0)) break;

@@ -122,21 +122,30 @@ def test_sst_files_verify_damaged(dev, oracle, native, files):
     np.testing.assert_array_equal(_u32(out2), want2)
 
 
-RING_CHUNKS = 16  # kRingChunks: spans of up to 16 chunks of 4 KiB are folded in the static ring
+RING_CHUNKS = 32  # kRingChunks: spans of up to 32 chunks of 4 KiB are folded in the static ring
+TICKET_LG_MIN = 2  # kTicketLgMin
+
+
+def ticket_lg(nch):
+    """crc32c_direct.hip's ticket_lg: the smallest 2^lg >= 2^TICKET_LG_MIN
+    chunks per ticket that keeps a span at <= 64 tickets."""
+    per = (nch + 63) // 64
+    lg = 0 if per <= 1 else (per - 1).bit_length()
+    return max(lg, TICKET_LG_MIN)
 
 
 def test_tickets_claimed_and_combined(dev, oracle, native):
-    """Long spans (more than 16 chunks) of every ticket size (1, 2, 4 and 8
-    chunks per ticket, up to 128 tickets: a two-step combine) mixed with
-    short and ring-folded multi-chunk ones, at odd offsets, random init, MASK;
-    the counters account for every ticket (claimed early, late or adopted)
-    and no span was folded whole."""
+    """Long spans (more than 32 chunks) of every ticket size from 4 to 256
+    chunks (<= 64 tickets per span) mixed with short and ring-folded
+    multi-chunk ones, at odd offsets, random init, MASK; the counters account
+    for every ticket (claimed early, late or adopted) and no span was folded
+    whole."""
     import torch
     from prismdb_amd import crc32c
 
     rng = np.random.default_rng(0x5EED00D3)
-    long_lens = [4097, 8192 + 5, 16 * 4096 + 3, 20 * 4096 + 11, 64 * 4096 - 5, 64 * 4096 + 1, 65 * 4096, 300_001,
-                 1 << 20, (4 << 20) + 3, 2 * 4096 * 64 + 7]
+    long_lens = [4097, 8192 + 5, 16 * 4096 + 3, 20 * 4096 + 11, 33 * 4096 + 9, 64 * 4096 - 5, 64 * 4096 + 1, 65 * 4096, 300_001,
+                 1 << 20, (4 << 20) + 3, 2 * 4096 * 64 + 7, (32 << 20) + 1001, (64 << 20) - 3]
     lens = np.concatenate([rng.integers(0, 4097, size=3000), long_lens]).astype(np.uint64)
     rng.shuffle(lens)
     gaps = rng.integers(0, 9, size=len(lens)).astype(np.uint64)
@@ -152,8 +161,7 @@ def test_tickets_claimed_and_combined(dev, oracle, native):
         nch = (W + 1023) // 1024
         if nch <= RING_CHUNKS:
             return 0
-        per = (nch + 63) // 64
-        lg = 0 if per <= 1 else 1 if per <= 2 else 2 if per <= 4 else 3
+        lg = ticket_lg(nch)
         return (nch + (1 << lg) - 1) >> lg
 
     buf = torch.empty(len(host) + 8, dtype=torch.uint8, device=dev)
@@ -174,7 +182,7 @@ def test_tickets_claimed_and_combined(dev, oracle, native):
 
 @pytest.mark.parametrize("mode", ["plain", "verify", "seal", "log_verify"])
 def test_ring_multichunk_spans(dev, oracle, native, mode):
-    """Spans of 2..16 chunks are folded by their run's wave in the static
+    """Spans of 2..32 chunks are folded by their run's wave in the static
     ring, chunk after chunk on one stream (no tickets: the counters do not
     move).  Every chunk count at lengths around the chunk boundaries, every
     start alignment, random init, mixed with one-chunk spans; verify against
@@ -188,7 +196,7 @@ def test_ring_multichunk_spans(dev, oracle, native, mode):
     for k in range(1, RING_CHUNKS + 1):
         for d in (-3, -1, 0, 1, 2, 5):
             L = k * 4096 + d
-            if 0 < L <= RING_CHUNKS * 4096 - 4:  # body <= 16 chunks at any alignment
+            if 0 < L <= RING_CHUNKS * 4096 - 4:  # body <= 32 chunks at any alignment
                 lens.append(L)
     lens = np.array(lens + rng.integers(0, 4097, size=400).tolist() +
                     rng.integers(4097, RING_CHUNKS * 4096 - 4, size=300).tolist(), dtype=np.uint64)
@@ -263,6 +271,49 @@ def test_ring_batch_of_16_64k_spans(dev, oracle, native):
     assert (_stats(native) - before).tolist() == [0, 0, 0, 0]
 
 
+def test_huge_spans_all_waves_claim(dev, oracle, native):
+    """A one-launch batch of a few 24-40 MiB spans at odd offsets among short
+    ones (a push of >= 1 MiB of ticket work calls every wave to claim): every
+    result against the oracle, every ticket accounted for once; verify mode
+    with one damaged huge span."""
+    import torch
+    from prismdb_amd import crc32c
+
+    rng = np.random.default_rng(0x5EED00E5)
+    lens = np.concatenate([rng.integers(0, 4097, size=2000),
+                           rng.integers(24 << 20, 40 << 20, size=5)]).astype(np.uint64)
+    rng.shuffle(lens)
+    off = np.cumsum(np.concatenate([[7], (lens + 4 + 3)[:-1]])).astype(np.uint64)
+    host = oracle.synth(int(off[-1] + lens[-1]) + 16, 0x5EED00E6)
+    raw, _ = oracle.batch(host, off, lens)
+    masked = np.array([oracle.mask(int(c)) for c in raw], dtype=np.uint32)
+    tr = (off + lens).astype(np.int64)[:, None] + np.arange(4)[None, :]
+    host[tr] = masked.astype("<u4").view(np.uint8).reshape(-1, 4)
+    big = int(np.argmax(lens))
+    host[int(off[big]) + int(lens[big]) // 2] ^= 0x02
+    want, wmm = oracle.batch(host, off, lens, verify=True)
+    buf = torch.from_numpy(host).to(dev)
+    d_off = torch.from_numpy(off.astype(np.int64)).to(dev)
+    d_len = torch.from_numpy(lens.astype(np.uint32).view(np.int32)).to(dev)
+    crc32c.batch(buf, d_off[:1], d_len[:1])
+    before = _stats(native)
+    out, mm = crc32c.batch(buf, d_off, d_len, verify=True)
+    after = _stats(native)
+    assert _last_split_rc(native) == -2
+    np.testing.assert_array_equal(_u32(out), want)
+    np.testing.assert_array_equal(mm.cpu().numpy(), wmm)
+    assert np.flatnonzero(wmm).tolist() == [big]
+    expect = 0
+    for L, o in zip(lens.tolist(), off.tolist()):
+        h = min((4 - o % 4) % 4, L)  # the device copy starts 256-B aligned
+        nch = ((L - h) // 4 + 1023) // 1024
+        if nch > RING_CHUNKS:
+            lg = ticket_lg(nch)
+            expect += (nch + (1 << lg) - 1) >> lg
+    d = after - before
+    assert d[1] == 0 and d[0] + d[2] + d[3] == expect, (d, expect)
+
+
 def test_ticket_workspace_full_whole_spans(dev, oracle, native):
     """A ticket workspace of 16 entries: the first pushes fit, the rest spill
     to whole-span folding by their discovering wave; claims of null tickets
@@ -322,8 +373,7 @@ def test_late_push_and_orphans(dev, oracle, native, dbg):
     assert (gmm == 0).all()
     d = after - before
     nch = (int(lens[-1]) + 4095) // 4096  # the index block (8-B aligned, offset multiple of 4)
-    per = (nch + 63) // 64
-    lg = 0 if per <= 1 else 1 if per <= 2 else 2 if per <= 4 else 3
+    lg = ticket_lg(nch)
     T = (nch + (1 << lg) - 1) >> lg
     assert d[0] + d[2] + d[3] == T, (d, T)
     assert d[1] == 0

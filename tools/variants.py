@@ -89,6 +89,22 @@ VARIANTS = {
     "lane_noseal": [("crc32c_kernels.hip",
                      '          asm volatile("global_store_dword %0, %1, off" : : "v"(ta), "v"(v) : "memory");\n',
                      '          (void)ta;\n')] + MEASURE_ONLY,
+    # the one-launch kernel's table fill retired after slot 0's first task
+    # only (17 loads in flight), the group barrier before the other two
+    # tasks of slot 0 are issued: issuing all 51 first held the barrier until
+    # the memory system had drained ~37 MB (~5 us)
+    "tables_after_st0": [("crc32c_direct.hip",
+                          "#pragma unroll\n    for (int st = 0; st < 3; ++st) issue(tk[0][st], wb[0][st], eb[0][st]);\n"
+                          "    tables_wait<3 * (kRounds + 1)>(tr);  // slot 0's 51 loads stay in flight\n"
+                          "    tables_store<kDirectThreads>(lds, tr, tid);\n"
+                          "    // Group barrier for the LDS image.  Not __syncthreads(): its release\n"
+                          "    // fence waits for every outstanding load (vmcnt(0)), slot 0's included.\n"
+                          "    asm volatile(\"s_waitcnt lgkmcnt(0)\\n\\ts_barrier\" ::: \"memory\");\n",
+                          "    issue(tk[0][0], wb[0][0], eb[0][0]);\n"
+                          "    tables_wait<kRounds + 1>(tr);\n"
+                          "    tables_store<kDirectThreads>(lds, tr, tid);\n"
+                          "    asm volatile(\"s_waitcnt lgkmcnt(0)\\n\\ts_barrier\" ::: \"memory\");\n"
+                          "#pragma unroll\n    for (int st = 1; st < 3; ++st) issue(tk[0][st], wb[0][st], eb[0][st]);\n")],
     # measurement: per-wave phase timestamps (s_memrealtime, 100 MHz) written
     # after the results: entry, descriptors in, tables in, first fold, ring
     # drained, exit (tools/direct_timeline.py reads them)
