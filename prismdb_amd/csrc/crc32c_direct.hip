@@ -647,31 +647,35 @@ __global__ __launch_bounds__(kDirectThreads) void crc32c_direct_kernel(SpanBatch
       // a stream's register between the chunks of its current span
       uint32_t carry[3] = {0u, 0u, 0u};
       auto fold = [&](const DTask (&t)[3], uint32_t (&w)[3][kRounds], const uint32_t (&e)[3]) {
+        // Per stream, unconditionally (three independent chains; under
+        // per-stream branches the head feeds and the realignments ran one
+        // after the other): the initial register, fed the head bytes, enters
+        // chunk 0 with its body word 0 (a zero injection for a later chunk,
+        // which continues its stream's carried register); every stream is
+        // realigned and reduced, and a span's last chunk finishes it.
         uint32_t r[3], acc[3];
 #pragma unroll
         for (int st = 0; st < 3; ++st) {
-          r[st] = 0u;
-          acc[st] = carry[st];
-          if (t[st].rc() == 0u) {
-            // initial register (init fed the head bytes) into body word 0
-            r[st] = feed_short(ss, lane, readlane(vinit, t[st].slot()) ^ kConditioning, edge_head(e[st], t[st].h()),
-                               t[st].h());
-            acc[st] = 0u;
-            if (t[st].z) inject(w[st], t[st].pad(), r[st]);
-          }
+          const bool c0 = t[st].rc() == 0u;
+          r[st] = feed_short(ss, lane, readlane(vinit, t[st].slot()) ^ kConditioning, edge_head(e[st], t[st].h()),
+                             t[st].h());
+          acc[st] = c0 ? 0u : carry[st];
+          if (t[st].z) inject(w[st], t[st].pad(), c0 ? r[st] : 0u);
         }
 #pragma unroll
         for (int j = 0; j < kRounds; ++j) {
 #pragma unroll
           for (int st = 0; st < 3; ++st) acc[st] = step256(lds, tab, acc[st], w[st][j]);
         }
+        uint32_t v[3];
+#pragma unroll
+        for (int st = 0; st < 3; ++st) v[st] = realign(lds, nibtab, acc[st]);
 #pragma unroll
         for (int st = 0; st < 3; ++st) {
           carry[st] = acc[st];
-          if (t[st].valid() && t[st].rlast()) {
-            const uint32_t bv = wave_xor(realign(lds, nibtab, acc[st]));
+          const uint32_t bv = wave_xor(v[st]);
+          if (t[st].valid() && t[st].rlast())
             finish(t[st], t[st].z ? bv : r[st], edge_tail(e[st], t[st].t()), edge_stored(e[st]), true);
-          }
         }
       };
       {
