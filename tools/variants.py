@@ -105,6 +105,15 @@ VARIANTS = {
                           "    tables_store<kDirectThreads>(lds, tr, tid);\n"
                           "    asm volatile(\"s_waitcnt lgkmcnt(0)\\n\\ts_barrier\" ::: \"memory\");\n"
                           "#pragma unroll\n    for (int st = 1; st < 3; ++st) issue(tk[0][st], wb[0][st], eb[0][st]);\n")],
+    # the sealing lane kernel's side load of a record's last task reads the
+    # dword holding its header crc (unused: HD is only read at task 0), so
+    # that the line is in L2 when the crc is stored
+    "lane_seal_touch": [("crc32c_kernels.hip",
+                         "    if (kSideAlways || t.k == 0) HD[sl] = asm_load_u32(owned && t.k == 0 ? vp & ~3ull : zero);\n",
+                         "    if (kSideAlways || t.k == 0)\n"
+                         "      HD[sl] = asm_load_u32(owned && t.k == 0 ? vp & ~3ull\n"
+                         "                            : (!kVerify && owned && lastk && (a.flags & kFlagWriteTrailer))\n"
+                         "                                  ? (hdr ? vp - kLogCrcBack : vp + vlen) & ~3ull : zero);\n")],
     # measurement: per-wave phase timestamps (s_memrealtime, 100 MHz) written
     # after the results: entry, descriptors in, tables in, first fold, ring
     # drained, exit (tools/direct_timeline.py reads them)
