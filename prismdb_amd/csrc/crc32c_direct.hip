@@ -10,17 +10,19 @@
 // (one 768-thread group: the tables take all of LDS):
 //
 //   static run   wave w < K owns q or q + 1 consecutive spans (<= 64; lane j
-//                holds span j's descriptor).  Its one-chunk spans (all the
-//                data blocks of an SST) go through an inline-asm ring of two
-//                slots x three streams -- stream st takes run positions st,
-//                st + 3, ..., so a fold reads three neighbouring blocks --
-//                with counted vmcnt waits and one coalesced store of the
-//                run's results.  At 12 waves per CU an SST file's ~5.5 spans
-//                per wave are all requested at once.
-//   long spans   (more than one 4 KiB chunk) are found by their run's wave
-//                first and cut into T tickets of g = 2^lg chunks (the smallest
-//                g <= 8 that gives T <= 64; ticket 0 takes the remainder).  The
-//                wave pushes all its tickets with ONE 64-bit atomic on
+//                holds span j's descriptor).  Its spans of up to kRingChunks
+//                (32) chunks of 4 KiB -- all the data blocks of an SST -- go
+//                through an inline-asm ring of two slots x three streams:
+//                stream st takes run positions st, st + 3, ..., so a fold
+//                reads three neighbouring blocks, and a span of several
+//                chunks is folded chunk after chunk on its stream (the
+//                register carried between tasks).  Counted vmcnt waits, one
+//                coalesced store of the run's results.  At 12 waves per CU an
+//                SST file's ~5.5 spans per wave are all requested at once.
+//   long spans   (more than kRingChunks chunks) are found by their run's wave
+//                first and cut into T <= 64 tickets of g = 2^lg chunks (lg in
+//                kTicketLgMin..14; ticket 0 takes the remainder).  The wave
+//                pushes all its tickets with ONE 64-bit atomic on
 //                word = supply << 32 | claimed and writes the ticket map
 //                (span | ticket index, span address, len, init: four 8-B
 //                words, each tagged with the call's tag, no fence).
@@ -32,9 +34,11 @@
 //                the first loads instead of on the kernel's tail.
 //   late claims  a wave that pushed tickets claims, after its own run, one at
 //                a time until none is left, so every pushed ticket is claimed
-//                by someone.  Other static waves just leave (3072 reads of
-//                `word` at the end cost ~8 us).
-//
+//                by someone.  Other static waves leave (3072 reads of `word`
+//                at the end cost ~8 us) unless a push of >= 1 MiB of ticket
+//                work set the help flag (32 tagged replicas); groups a small
+//                batch leaves idle wait ~3 us for that flag too.
+
 // A claim is one atomicAdd of 1 on the claimed half of `word`: ticket C below
 // the supply S is the claimer's.  A claim at C >= S ("orphan": two workers
 // raced for the last visible ticket) belongs to whoever pushes ticket C: the
@@ -46,7 +50,8 @@
 // writes back the XCD's L2 and, like an acquire, waits for every load in
 // flight -- at the push, the table fill).  A ticket folds
 // its chunks into a partial register R_k (ticket 0 from the span's initial
-// register, the others from 0) with compiler-scheduled buffer loads; the wave
+// register, the others from 0) with compiler-scheduled buffer loads, the next
+// two chunks' loads in flight during a fold; the wave
 // that finishes a span's last ticket (per-span counter) combines
 // R = sum_k M^(T-1-k) R_k, M = shift_{4 KiB g}, lane-parallel as
 // crc32c_combine_kernel does, feeds the tail bytes and stores the result.
