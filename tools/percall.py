@@ -12,8 +12,9 @@ one stream.
 
 for the one-launch path (the default for <= 2^17 spans) and, pinned by the
 test hook, the planner path; seal (MASK | WRITE_TRAILER), verify and plain,
-and seal / verify with PRISMDB_CRC32C_UNORDERED alternating between two
-files (every other launch may overlap its predecessor).
+seal / verify with PRISMDB_CRC32C_UNORDERED alternating between two
+files (every other launch may overlap its predecessor), and seal / verify
+rotating over eight distinct files (540 MB: not served from the MALL).
 Prints one JSON object."""
 import ctypes
 import json
@@ -39,12 +40,24 @@ def main():
     buf = torch.empty(size, dtype=torch.uint8, device=dev)
     crc32c.fill_synthetic(buf, 0x5EED00F1)
     buf2 = buf.clone()  # a second file: unordered calls alternate between the two
+    # eight distinct files (540 MB, over the 256 MB MALL): a compaction's
+    # files are new data, while back-to-back calls on one file are partly
+    # served from the MALL (profiles/r03ad_pmc_per_span.json)
+    files = [torch.empty_like(buf) for _ in range(8)]
+    for i, f in enumerate(files):
+        crc32c.fill_synthetic(f, 0x5EED0100 + i)
+    rot = [0]
+
+    def next_file():
+        rot[0] = (rot[0] + 1) % len(files)
+        return files[rot[0]]
     off = np.concatenate([np.arange(nd, dtype=np.int64) * 3992, [nd * 3992]])
     lens = np.array([3988] * nd + [486977], dtype=np.int32)
     d_off = torch.from_numpy(off).to(dev)
     d_len = torch.from_numpy(lens).to(dev)
     out = torch.empty(nd + 1, dtype=torch.int32, device=dev)
     mm = torch.empty(nd + 1, dtype=torch.uint8, device=dev)
+    mm2 = torch.empty(nd + 1, dtype=torch.uint8, device=dev)
     crc32c.batch(buf, d_off, d_len, mask=True, trailer=True)  # seal once: verify then passes
     crc32c.batch(buf2, d_off, d_len, mask=True, trailer=True)
     flip = [0]
@@ -88,6 +101,11 @@ def main():
         "verify": lambda: crc32c.batch(buf, d_off, d_len, verify=True, out=out, mismatch=mm, check_bounds=False),
         "plain": lambda: crc32c.batch(buf, d_off, d_len, out=out, check_bounds=False),
         "data_only": lambda: crc32c.batch(buf, d_off[:nd], d_len[:nd], out=out[:nd], check_bounds=False),
+        # seal / verify (the stored trailers do not match: results only) over eight distinct files in turn
+        "seal_distinct": lambda: crc32c.batch(next_file(), d_off, d_len, mask=True, trailer=True, out=out,
+                                              check_bounds=False),
+        "verify_distinct": lambda: crc32c.batch(next_file(), d_off, d_len, verify=True, out=out, mismatch=mm2,
+                                                check_bounds=False),
         # PRISMDB_CRC32C_UNORDERED: consecutive calls on two different files
         "seal_unordered": lambda: crc32c.batch(other(), d_off, d_len, mask=True, trailer=True, out=out,
                                                check_bounds=False, unordered=True),
@@ -117,6 +135,8 @@ def main():
     res["one_launch_tickets_per_call"] = dict(zip(("adopted", "whole", "worker", "late"),
                                                   [round((b - a) / 200, 2) for a, b in zip(s0, st)]))
     res["fixed_data_blocks_back_to_back_us"] = b2b(lambda: crc32c.batch_fixed(buf, 3992, 3988, nd, out=out[:nd]))
+    res["fixed_data_blocks_distinct_back_to_back_us"] = b2b(
+        lambda: crc32c.batch_fixed(next_file(), 3992, 3988, nd, out=out[:nd]))
     res["ideal_us_at_8TBps"] = round(res["bytes"] / 8e12 * 1e6, 2)
     res["ideal_us_at_6.5TBps"] = round(res["bytes"] / 6.5e12 * 1e6, 2)
     print(json.dumps(res))

@@ -114,6 +114,9 @@ VARIANTS = {
                          "      HD[sl] = asm_load_u32(owned && t.k == 0 ? vp & ~3ull\n"
                          "                            : (!kVerify && owned && lastk && (a.flags & kFlagWriteTrailer))\n"
                          "                                  ? (hdr ? vp - kLogCrcBack : vp + vlen) & ~3ull : zero);\n")],
+    # span / fixed kernels at 12 and 8 waves per CU (768- / 512-thread groups)
+    "waves12": [("crc32c_device.h", "constexpr int kWavesPerGroup = 16;", "constexpr int kWavesPerGroup = 12;")],
+    "waves8": [("crc32c_device.h", "constexpr int kWavesPerGroup = 16;", "constexpr int kWavesPerGroup = 8;")],
     # measurement: per-wave phase timestamps (s_memrealtime, 100 MHz) written
     # after the results: entry, descriptors in, tables in, first fold, ring
     # drained, exit (tools/direct_timeline.py reads them)
