@@ -20,7 +20,8 @@
 //                coalesced store of the run's results.  At 12 waves per CU an
 //                SST file's ~5.5 spans per wave are all requested at once.
 //   long spans   (more than kRingChunks chunks) are found by their run's wave
-//                first and cut into T <= 64 tickets of g = 2^lg chunks (lg in
+//                first and cut into T tickets of g = 2^lg chunks (T <= 64, or
+//                up to 4096 when the batch has fewer spans than waves; lg in
 //                kTicketLgMin..14; ticket 0 takes the remainder).  The wave
 //                pushes all its tickets with ONE 64-bit atomic on
 //                word = supply << 32 | claimed and writes the ticket map
@@ -72,14 +73,22 @@ namespace dev {
 
 namespace {
 
+// ceil(log2(x)) for x >= 1
+__device__ __forceinline__ uint32_t ceil_lg(uint32_t x) { return x <= 1u ? 0u : 32u - (uint32_t)__builtin_clz(x - 1u); }
 // Chunks per ticket: 2^lg, the smallest power of two that keeps a span at
-// <= 64 tickets (one Horner step in the combine; any span of < 4 GiB), and
-// at least 2^kTicketLgMin.  Tickets were <= 8 chunks: a 64 MiB span was
-// 2048 tickets, and 127 such spans took 26 ms through 96 ticket workers.
+// <= 2^lt tickets, and at least 2^kTicketLgMin.  2^lt = 64 (one Horner step
+// in the combine) unless the batch has far fewer spans than waves: then
+// ~2 nwaves / n (floor(log2(2 nwaves)) - ceil(log2(n)), up to 4096), so that
+// a few huge spans still give every wave tickets (one 1 GiB span as 64
+// tickets of 16 MiB kept 64 waves busy for 4.2 ms).  Tickets were <= 8
+// chunks in round 3's first version: a 64 MiB span was 2048 tickets, and
+// 127 such spans took 26 ms through 96 ticket workers.  Pusher and claimer
+// compute it from the same (nch, n); no division.
 constexpr uint32_t kTicketLgMin = 2;
-__device__ __forceinline__ uint32_t ticket_lg(uint32_t nch) {
-  const uint32_t per = (nch + 63u) >> 6;  // ceil(nch / 64) >= 1
-  const uint32_t lg = per <= 1u ? 0u : 32u - (uint32_t)__builtin_clz(per - 1u);  // ceil(log2(per))
+__device__ __forceinline__ uint32_t ticket_lg(uint32_t nch, uint32_t n, uint32_t nwaves) {
+  const int32_t l = (int32_t)(31u - (uint32_t)__builtin_clz(2u * nwaves)) - (int32_t)ceil_lg(n);
+  const uint32_t lt = l < 6 ? 6u : (l > 12 ? 12u : (uint32_t)l);
+  const uint32_t lg = ceil_lg((nch + (1u << lt) - 1u) >> lt);
   return lg < kTicketLgMin ? kTicketLgMin : lg;
 }
 static_assert(kTicketLgMax >= 14, "2^20 chunks (4 GiB) in 64 tickets");
@@ -264,7 +273,7 @@ __global__ __launch_bounds__(kDirectThreads) void crc32c_direct_kernel(SpanBatch
     const bool lng = lane < m && g.c1 > kRingChunks;
     uint32_t T = 0, lg = 0;
     if (lng) {
-      lg = ticket_lg(g.c1);
+      lg = ticket_lg(g.c1, n, nwaves);
       T = (g.c1 + (1u << lg) - 1u) >> lg;
     }
     lm = __ballot(lng);
@@ -282,6 +291,13 @@ __global__ __launch_bounds__(kDirectThreads) void crc32c_direct_kernel(SpanBatch
                                      __HIP_MEMORY_SCOPE_AGENT);
       const uint32_t S0 = readlane((uint32_t)(old >> 32), 0), C0 = readlane((uint32_t)old, 0);
       if ((uint64_t)S0 + total <= d.cap) {
+        // A large push (>= kHelpChunks of ticket work) calls every wave to
+        // claim after its run (the 96-256 ticket workers alone took 26 ms
+        // over 127 spans of 64 MiB).  Set before the map is written (a
+        // claimer polls its entry until it is): idle groups wait for the
+        // flag only ~3 us, and a push of 4096 entries takes longer.
+        if (chunks >= kHelpChunks && lane < 32u)
+          __hip_atomic_store(d.help + 32u * lane, d.tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         // the ticket map, one long span at a time, 64 entries per step: four
         // tagged words each, in any order (a claimer polls until all four
         // carry this call's tag; no fence, so the push does not wait for the
@@ -303,11 +319,6 @@ __global__ __launch_bounds__(kDirectThreads) void crc32c_direct_kernel(SpanBatch
             put_tagged(e + 3, d.tag, in);
           }
         }
-        // A large push (>= kHelpChunks of ticket work) calls every wave to
-        // claim after its run: the 96-256 ticket workers alone took 26 ms
-        // over 127 spans of 64 MiB.
-        if (chunks >= kHelpChunks && lane < 32u)
-          __hip_atomic_store(d.help + 32u * lane, d.tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (C0 > S0) {
           adopt_lo = S0;
           adopt_hi = C0 < S0 + total ? C0 : S0 + total;
@@ -582,7 +593,7 @@ __global__ __launch_bounds__(kDirectThreads) void crc32c_direct_kernel(SpanBatch
       const uint64_t addr = ((uint64_t)(readlane((uint32_t)(ew >> 32), 1) & 0xFFFFu) << 32) | readlane((uint32_t)ew, 1);
       DTask t = geometry(addr, readlane((uint32_t)ew, 2));
       t.b = sb;
-      const uint32_t lg = ticket_lg(t.c1), T = (t.c1 + (1u << lg) - 1u) >> lg, f0 = tkt - k;
+      const uint32_t lg = ticket_lg(t.c1, n, nwaves), T = (t.c1 + (1u << lg) - 1u) >> lg, f0 = tkt - k;
       const uint32_t first = t.c1 - ((T - 1u) << lg);  // ticket 0: the remainder
       t.c = k ? first + ((k - 1u) << lg) : 0u;
       t.c1 = k ? t.c + (1u << lg) : first;

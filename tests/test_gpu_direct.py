@@ -126,12 +126,23 @@ RING_CHUNKS = 32  # kRingChunks: spans of up to 32 chunks of 4 KiB are folded in
 TICKET_LG_MIN = 2  # kTicketLgMin
 
 
-def ticket_lg(nch):
+def nwaves():
+    """The one-launch kernel's waves: 12 per CU."""
+    import torch
+
+    return 12 * torch.cuda.get_device_properties(0).multi_processor_count
+
+
+def _ceil_lg(x):
+    return 0 if x <= 1 else (x - 1).bit_length()
+
+
+def ticket_lg(nch, n):
     """crc32c_direct.hip's ticket_lg: the smallest 2^lg >= 2^TICKET_LG_MIN
-    chunks per ticket that keeps a span at <= 64 tickets."""
-    per = (nch + 63) // 64
-    lg = 0 if per <= 1 else (per - 1).bit_length()
-    return max(lg, TICKET_LG_MIN)
+    chunks per ticket that keeps a span at <= 2^lt tickets, lt =
+    floor(log2(2 nwaves)) - ceil(log2(n)) clamped to 6..12."""
+    lt = min(12, max(6, (2 * nwaves()).bit_length() - 1 - _ceil_lg(n)))
+    return max(_ceil_lg((nch + (1 << lt) - 1) >> lt), TICKET_LG_MIN)
 
 
 def test_tickets_claimed_and_combined(dev, oracle, native):
@@ -161,7 +172,7 @@ def test_tickets_claimed_and_combined(dev, oracle, native):
         nch = (W + 1023) // 1024
         if nch <= RING_CHUNKS:
             return 0
-        lg = ticket_lg(nch)
+        lg = ticket_lg(nch, len(lens))
         return (nch + (1 << lg) - 1) >> lg
 
     buf = torch.empty(len(host) + 8, dtype=torch.uint8, device=dev)
@@ -308,10 +319,49 @@ def test_huge_spans_all_waves_claim(dev, oracle, native):
         h = min((4 - o % 4) % 4, L)  # the device copy starts 256-B aligned
         nch = ((L - h) // 4 + 1023) // 1024
         if nch > RING_CHUNKS:
-            lg = ticket_lg(nch)
+            lg = ticket_lg(nch, len(lens))
             expect += (nch + (1 << lg) - 1) >> lg
     d = after - before
     assert d[1] == 0 and d[0] + d[2] + d[3] == expect, (d, expect)
+
+
+@pytest.mark.parametrize("nspans", [1, 3])
+def test_few_huge_spans_many_tickets(dev, oracle, native, nspans):
+    """Batches of one 320 MiB span and of three ~100 MiB spans: fewer spans
+    than waves, so a span gets up to 2 nwaves / n tickets (<= 4096; several
+    Horner steps in the combine), claimed by every wave.  Results against
+    the oracle, every ticket accounted for once."""
+    import torch
+    from prismdb_amd import crc32c
+
+    rng = np.random.default_rng(0x5EED00E7 + nspans)
+    if nspans == 1:
+        lens = np.array([(320 << 20) + 13], dtype=np.uint64)
+    else:
+        lens = rng.integers(90 << 20, 110 << 20, size=nspans).astype(np.uint64)
+    off = np.cumsum(np.concatenate([[5], (lens + 3)[:-1]])).astype(np.uint64)
+    host = oracle.synth(int(off[-1] + lens[-1]) + 16, 0x5EED00E8)
+    init = rng.integers(0, 2**32, size=nspans, dtype=np.uint64).astype(np.uint32)
+    want, _ = oracle.batch(host, off, lens, init, mask=True)
+    buf = torch.from_numpy(host).to(dev)
+    d_off = torch.from_numpy(off.astype(np.int64)).to(dev)
+    d_len = torch.from_numpy(lens.astype(np.uint32).view(np.int32)).to(dev)
+    d_init = torch.from_numpy(init.view(np.int32)).to(dev)
+    crc32c.batch(buf, d_off[:1], d_len[:1])
+    before = _stats(native)
+    out, _ = crc32c.batch(buf, d_off, d_len, d_init, mask=True)
+    after = _stats(native)
+    assert _last_split_rc(native) == -2
+    np.testing.assert_array_equal(_u32(out), want)
+    expect = 0
+    for L, o in zip(lens.tolist(), off.tolist()):
+        h = min((4 - o % 4) % 4, L)
+        nch = ((L - h) // 4 + 1023) // 1024
+        lg = ticket_lg(nch, nspans)
+        expect += (nch + (1 << lg) - 1) >> lg
+    d = after - before
+    assert d[1] == 0 and d[0] + d[2] + d[3] == expect, (d, expect)
+    assert expect > 64 * nspans  # more than one Horner step per span
 
 
 def test_ticket_workspace_full_whole_spans(dev, oracle, native):
@@ -373,7 +423,7 @@ def test_late_push_and_orphans(dev, oracle, native, dbg):
     assert (gmm == 0).all()
     d = after - before
     nch = (int(lens[-1]) + 4095) // 4096  # the index block (8-B aligned, offset multiple of 4)
-    lg = ticket_lg(nch)
+    lg = ticket_lg(nch, len(lens))
     T = (nch + (1 << lg) - 1) >> lg
     assert d[0] + d[2] + d[3] == T, (d, T)
     assert d[1] == 0

@@ -117,6 +117,11 @@ VARIANTS = {
     # span / fixed kernels at 12 and 8 waves per CU (768- / 512-thread groups)
     "waves12": [("crc32c_device.h", "constexpr int kWavesPerGroup = 16;", "constexpr int kWavesPerGroup = 12;")],
     "waves8": [("crc32c_device.h", "constexpr int kWavesPerGroup = 16;", "constexpr int kWavesPerGroup = 8;")],
+    # the one-launch kernel's ticket sizing without the batch-size term (<= 64 tickets per span)
+    "tlg64": [("crc32c_direct.hip",
+               "  const int32_t l = (int32_t)(31u - (uint32_t)__builtin_clz(2u * nwaves)) - (int32_t)ceil_lg(n);\n"
+               "  const uint32_t lt = l < 6 ? 6u : (l > 12 ? 12u : (uint32_t)l);\n",
+               "  (void)n;\n  (void)nwaves;\n  const uint32_t lt = 6u;\n")],
     # measurement: per-wave phase timestamps (s_memrealtime, 100 MHz) written
     # after the results: entry, descriptors in, tables in, first fold, ring
     # drained, exit (tools/direct_timeline.py reads them)
@@ -243,7 +248,8 @@ def do_run(args, names):
     nh = min(256, (args.gib << 30) // (64 << 20) - 1)
     hoff_ = torch.arange(nh, dtype=torch.int64, device=dev) * (64 << 20) + 1
     hlen_ = torch.full((nh,), (64 << 20) - 5, dtype=torch.int32, device=dev)
-    hout = torch.empty(nh, dtype=torch.int32, device=dev)
+    hout = torch.empty(max(nh, 1), dtype=torch.int32, device=dev)
+    h1len = torch.full((1,), (1 << 30) - 3, dtype=torch.int32, device=dev)
     al = rng.integers(0, 70000, size=(args.gib << 30) // 35000 // 2).astype(np.int64)
     ao = np.sort(rng.integers(0, (args.gib << 30) // 2 - 70001, size=len(al))).astype(np.int64)
     aoff, alen = torch.from_numpy(ao).to(dev), torch.from_numpy(al.astype(np.int32)).to(dev)
@@ -283,6 +289,9 @@ def do_run(args, names):
                                            fout.data_ptr(), None, 0, sp), nfd * (3988 + 16) + 486977 + 16),
         "file_verify": (lambda n: libs[n][1](buf.data_ptr(), foff.data_ptr(), flen.data_ptr(), None, nfd + 1,
                                              fout.data_ptr(), fmm.data_ptr(), 0, sp), nfd * (3988 + 17) + 486977 + 17),
+        # one span of 1 GiB - 3 B at an odd offset: the one-launch path's few-huge-spans case
+        "one_huge": (lambda n: libs[n][1](buf.data_ptr(), hoff_.data_ptr(), h1len.data_ptr(), None, 1,
+                                          hout.data_ptr(), None, 0, sp), (1 << 30) - 3 + 16),
         # one 4 KiB span: the per-call floor of the one-launch path
         "tiny_desc": (lambda n: libs[n][1](buf.data_ptr(), off4k.data_ptr(), len4k.data_ptr(), None, 1,
                                            fout.data_ptr(), None, 0, sp), 4096 + 16),
@@ -302,7 +311,8 @@ def do_run(args, names):
         work = {w: v for w, v in work.items() if w in args.work}
     res = {w: {n: [] for n in names} for w in work}
     agree = {}
-    outs_of = {"wal": wout, "wal_seal": wout, "sst3988": sout, "huge64m": hout, "file_fixed": fout, "file_desc": fout,
+    outs_of = {"wal": wout, "wal_seal": wout, "sst3988": sout, "huge64m": hout, "one_huge": hout, "file_fixed": fout,
+               "file_desc": fout,
                "file_verify": fout, "tiny_desc": fout}
     for w, (fn, _) in work.items():
         ref = None
