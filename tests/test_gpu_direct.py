@@ -590,3 +590,77 @@ def test_unordered_file_calls(dev, oracle, native):
     np.testing.assert_array_equal(got[2, per:2 * per], raw[:per])
     assert not mms.cpu().numpy()[0].any() and not mms.cpu().numpy()[1, :per].any()
     assert (buf.cpu().numpy() == sealed).all()  # every trailer as the reference writes it
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_direct_random_batches(dev, oracle, native, seed):
+    """Random one-launch batches: 1 to 20 000 spans mixing every length class
+    the kernel treats differently -- empty and short spans, ring spans of 2
+    to 32 chunks, ticket spans (33 chunks to a few MiB), now and then one or
+    two of tens of MiB (help flag, idle groups claiming, batch-scaled
+    tickets) -- at any alignment, in a random mode: plain with init, MASK,
+    verify (a few damaged), or sealing.  Every result against the oracle,
+    every ticket accounted for exactly once."""
+    import torch
+    from prismdb_amd import crc32c
+
+    rng = np.random.default_rng(0x5EED0F00 + seed)
+    n = int(rng.choice([1, 2, 5, 40, 300, 3000, 20000]))
+    p = [0.55, 0.2, 0.15, 0.09, 0.01] if n < 3000 else [0.8, 0.16, 0.035, 0.005, 0.0]
+    cls = rng.choice(5, size=n, p=p)
+    lens = np.where(cls == 0, rng.integers(0, 4097, size=n),
+           np.where(cls == 1, rng.integers(4097, RING_CHUNKS * 4096 - 4, size=n),
+           np.where(cls == 2, rng.integers(RING_CHUNKS * 4096, 1 << 20, size=n),
+           np.where(cls == 3, rng.integers(1 << 20, 4 << 20, size=n),
+                    rng.integers(16 << 20, 40 << 20, size=n))))).astype(np.uint64)
+    while int(lens.sum()) > (400 << 20):  # keep the case small: shrink the largest span
+        lens[int(np.argmax(lens))] //= 4
+    mode = ["plain", "mask", "verify", "seal"][int(rng.integers(0, 4))]
+    gaps = rng.integers(4, 12, size=n).astype(np.uint64)
+    off = np.cumsum(np.concatenate([[int(rng.integers(0, 8))], (lens + gaps)[:-1]])).astype(np.uint64)
+    host = oracle.synth(int(off[-1] + lens[-1]) + 16, 0x5EED0F80 + seed)
+    init = rng.integers(0, 2**32, size=n, dtype=np.uint64).astype(np.uint32) if mode == "plain" else None
+    raw, _ = oracle.batch(host, off, lens)
+    masked = np.array([oracle.mask(int(c)) for c in raw], dtype=np.uint32)
+    if mode == "verify":
+        tr = (off + lens).astype(np.int64)[:, None] + np.arange(4)[None, :]
+        host[tr] = masked.astype("<u4").view(np.uint8).reshape(-1, 4)
+        for v in rng.choice(n, size=min(n, 3), replace=False):
+            if lens[v]:
+                host[int(off[v]) + int(rng.integers(0, int(lens[v])))] ^= 0x10
+        raw, _ = oracle.batch(host, off, lens)
+    buf = torch.from_numpy(host).to(dev)
+    d_off = torch.from_numpy(off.astype(np.int64)).to(dev)
+    d_len = torch.from_numpy(lens.astype(np.uint32).view(np.int32)).to(dev)
+    d_init = torch.from_numpy(init.view(np.int32)).to(dev) if init is not None else None
+    crc32c.batch(buf, d_off[:1], d_len[:1])
+    before = _stats(native)
+    if mode == "plain":
+        want, _ = oracle.batch(host, off, lens, init)
+        out, _ = crc32c.batch(buf, d_off, d_len, d_init)
+        np.testing.assert_array_equal(_u32(out), want)
+    elif mode == "mask":
+        out, _ = crc32c.batch(buf, d_off, d_len, mask=True)
+        np.testing.assert_array_equal(_u32(out), masked)
+    elif mode == "verify":
+        want, wmm = oracle.batch(host, off, lens, verify=True)
+        out, mm = crc32c.batch(buf, d_off, d_len, verify=True)
+        np.testing.assert_array_equal(_u32(out), want)
+        np.testing.assert_array_equal(mm.cpu().numpy(), wmm)
+    else:
+        out, _ = crc32c.batch(buf, d_off, d_len, mask=True, trailer=True)
+        np.testing.assert_array_equal(_u32(out), masked)
+        got = buf.cpu().numpy()
+        tr = (off + lens).astype(np.int64)[:, None] + np.arange(4)[None, :]
+        np.testing.assert_array_equal(got[tr].reshape(-1).view("<u4"), masked)
+    after = _stats(native)
+    assert _last_split_rc(native) == -2
+    expect = 0
+    for L, o in zip(lens.tolist(), off.tolist()):
+        h = min((4 - o % 4) % 4, L)  # the device copy starts 256-B aligned
+        nch = ((L - h) // 4 + 1023) // 1024
+        if nch > RING_CHUNKS:
+            lg = ticket_lg(nch, n)
+            expect += (nch + (1 << lg) - 1) >> lg
+    d = after - before
+    assert d[1] == 0 and d[0] + d[2] + d[3] == expect, (d, expect, n, mode)
