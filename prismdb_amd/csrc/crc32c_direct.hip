@@ -267,9 +267,18 @@ __global__ __launch_bounds__(kDirectThreads) void crc32c_direct_kernel(SpanBatch
   uint32_t adopt_lo = 0, adopt_hi = 0;  // orphans of this wave's push: its own to do
   uint64_t whole = 0;                   // workspace full: these run spans are folded whole here
   uint64_t lm = 0;                      // the run's long spans
+  // lane j's span geometry, computed here once for the whole run on the
+  // vector unit: the ring's tasks read it with four readlanes instead of
+  // redoing it on the scalar unit per task (body, body bytes, flags with
+  // the chunk count; only ring spans use the count)
+  uint32_t gb_lo = 0, gb_hi = 0, gz = 0, gf = 0;
   {
     const uint64_t p = base + (((uint64_t)voff_hi << 32) | voff_lo);
     const DTask g = geometry(p, vlen);
+    gb_lo = (uint32_t)g.body;
+    gb_hi = (uint32_t)(g.body >> 32);
+    gz = g.z;
+    gf = g.f | (((g.c1 - 1u) & 31u) << 27);
     const bool lng = lane < m && g.c1 > kRingChunks;
     uint32_t T = 0, lg = 0;
     if (lng) {
@@ -363,10 +372,11 @@ __global__ __launch_bounds__(kDirectThreads) void crc32c_direct_kernel(SpanBatch
         return t;
       }
       const uint32_t p = (uint32_t)__builtin_ctzll(avail);
-      const uint64_t off = ((uint64_t)readlane(voff_hi, p) << 32) | readlane(voff_lo, p);
-      DTask t = geometry(base + off, readlane(vlen, p));
+      DTask t;
+      t.body = ((uint64_t)readlane(gb_hi, p) << 32) | readlane(gb_lo, p);
+      t.z = readlane(gz, p);
+      t.f = readlane(gf, p) | (kKindStatic << 14) | (p << 16);  // (nch <= kRingChunks)
       t.b = sbase + p;
-      t.f |= (kKindStatic << 14) | (p << 16) | ((t.c1 - 1u) << 27);  // (nch <= kRingChunks)
       t.c = 0;  // (the ring reads the chunk from f)
       t.c1 = 1;
       j = p + 3u;
