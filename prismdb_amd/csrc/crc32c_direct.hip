@@ -470,7 +470,10 @@ __global__ __launch_bounds__(kDirectThreads) void crc32c_direct_kernel(SpanBatch
         if (a.out != nullptr) a.out[t.b] = v;
         if (kVerify && a.mismatch != nullptr) a.mismatch[t.b] = (uint8_t)mm;
       }
-      if ((a.flags & kFlagWriteTrailer) && lane == 0) {
+      // (a ring span's trailer is stored with the run's results, after the
+      // ring: a store between the slots' loads sits in the in-order vmcnt,
+      // and the counted waits would wait for its write acknowledgement)
+      if ((a.flags & kFlagWriteTrailer) && lane == 0 && !to_run) {
         const uint64_t start = t.body - t.h();
         store_le32(reinterpret_cast<const uint8_t*>(hdr ? start - kLogCrcBack : t.body + t.z + tl), v);
       }
@@ -793,6 +796,11 @@ __global__ __launch_bounds__(kDirectThreads) void crc32c_direct_kernel(SpanBatch
     if (lane < m && have != 0u) {
       if (a.out != nullptr) __builtin_nontemporal_store(res, a.out + sbase + lane);
       if (kVerify && a.mismatch != nullptr) __builtin_nontemporal_store((uint8_t)bad, a.mismatch + sbase + lane);
+      if (!kVerify && (a.flags & kFlagWriteTrailer)) {  // each lane its span's stored crc
+        const uint64_t p = base + (((uint64_t)voff_hi << 32) | voff_lo);
+        const uint64_t body = ((uint64_t)gb_hi << 32) | gb_lo;
+        store_le32(reinterpret_cast<const uint8_t*>(hdr ? p - kLogCrcBack : body + gz + ((gf >> 12) & 3u)), res);
+      }
     }
   }
 

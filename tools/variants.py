@@ -260,7 +260,7 @@ def do_run(args, names):
     flen = torch.from_numpy(np.concatenate([np.full(nfd, 3988, dtype=np.int32), [486977]]).astype(np.int32)).to(dev)
     fout = torch.empty(nfd + 1, dtype=torch.int32, device=dev)
     fmm = torch.empty(nfd + 1, dtype=torch.uint8, device=dev)
-    calls = {"file_fixed": 50, "file_desc": 50, "file_verify": 50, "tiny_desc": 50}
+    calls = {"file_fixed": 50, "file_desc": 50, "file_seal": 50, "file_verify": 50, "tiny_desc": 50}
     work = {
         "fixed4k": (lambda n: libs[n][0](buf.data_ptr(), 4096, 4096, nblk, 0, out.data_ptr(), None, 0, sp),
                     nblk * 4100),
@@ -287,6 +287,8 @@ def do_run(args, names):
                        nfd * (3988 + 4)),
         "file_desc": (lambda n: libs[n][1](buf.data_ptr(), foff.data_ptr(), flen.data_ptr(), None, nfd + 1,
                                            fout.data_ptr(), None, 0, sp), nfd * (3988 + 16) + 486977 + 16),
+        "file_seal": (lambda n: libs[n][1](buf.data_ptr(), foff.data_ptr(), flen.data_ptr(), None, nfd + 1,
+                                           fout.data_ptr(), None, 0x3, sp), nfd * (3988 + 16) + 486977 + 16),
         "file_verify": (lambda n: libs[n][1](buf.data_ptr(), foff.data_ptr(), flen.data_ptr(), None, nfd + 1,
                                              fout.data_ptr(), fmm.data_ptr(), 0, sp), nfd * (3988 + 17) + 486977 + 17),
         # one span of 1 GiB - 3 B at an odd offset: the one-launch path's few-huge-spans case
@@ -312,7 +314,7 @@ def do_run(args, names):
     res = {w: {n: [] for n in names} for w in work}
     agree = {}
     outs_of = {"wal": wout, "wal_seal": wout, "sst3988": sout, "huge64m": hout, "one_huge": hout, "file_fixed": fout,
-               "file_desc": fout,
+               "file_desc": fout, "file_seal": fout,
                "file_verify": fout, "tiny_desc": fout}
     for w, (fn, _) in work.items():
         ref = None
