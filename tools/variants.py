@@ -279,6 +279,9 @@ def do_run(args, names):
                      int(hlen.sum() + len(hlen)) * nf + nw * (4 + 4 + 12)),
         "sst3988": (lambda n: libs[n][1](buf.data_ptr(), soff.data_ptr(), slen.data_ptr(), None, ns,
                                          sout.data_ptr(), None, 0, sp), ns * (3988 + 4 + 12)),
+        # the same spans sealed (MASK | WRITE_TRAILER): the planner path's trailer stores
+        "sst3988_seal": (lambda n: libs[n][1](buf.data_ptr(), soff.data_ptr(), slen.data_ptr(), None, ns,
+                                              sout.data_ptr(), None, 0x3, sp), ns * (3988 + 4 + 12)),
         "huge64m": (lambda n: libs[n][1](buf.data_ptr(), hoff_.data_ptr(), hlen_.data_ptr(), None, nh,
                                          hout.data_ptr(), None, 0, sp), nh * ((64 << 20) - 5 + 16)),
         "adversarial": (lambda n: libs[n][1](buf.data_ptr(), aoff.data_ptr(), alen.data_ptr(), None, len(al),
@@ -313,7 +316,7 @@ def do_run(args, names):
         work = {w: v for w, v in work.items() if w in args.work}
     res = {w: {n: [] for n in names} for w in work}
     agree = {}
-    outs_of = {"wal": wout, "wal_seal": wout, "sst3988": sout, "huge64m": hout, "one_huge": hout, "file_fixed": fout,
+    outs_of = {"wal": wout, "wal_seal": wout, "sst3988": sout, "sst3988_seal": sout, "huge64m": hout, "one_huge": hout, "file_fixed": fout,
                "file_desc": fout, "file_seal": fout,
                "file_verify": fout, "tiny_desc": fout}
     for w, (fn, _) in work.items():
