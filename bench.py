@@ -10,9 +10,13 @@ base 256-B aligned.  One step = one pass of the engine over the whole batch
 RCCL gather of the 4-byte results to rank 0 (overlapped with the next pass on
 RCCL's own stream; the last one is inside the timed region).
 N > 1 runs one process per GPU under torch.distributed.run (weak scaling: each
-rank owns a different 64 GiB slice of the global block stream).  --strong keeps
-the total fixed instead (--nblocks blocks in all, nblocks / N per rank; SURVEY
-8(d) config 5), and --no-gather drops the RCCL gather (config 5 asks for both).
+rank owns a different 64 GiB slice of the global block stream).  Started as
+`python bench.py --gpus N` without a launcher (no WORLD_SIZE), bench starts
+torch.distributed.run itself with N ranks before anything touches the GPU and
+exits with its status; a WORLD_SIZE that disagrees with --gpus is an error.
+--strong keeps the total fixed instead (--nblocks blocks in all, nblocks / N
+per rank), and --no-gather drops the RCCL gather
+(config 5 asks for both).
 
 Printed (rank 0): ONE JSON line with the driver's contract fields plus
   roofline      dominant kernel vs the HBM roofline (HIP events on the launch stream)
@@ -26,6 +30,13 @@ Printed (rank 0): ONE JSON line with the driver's contract fields plus
                 through the descriptor path, results gathered to rank 0 over
                 RCCL (N > 1); its own GiB/s, never the headline value
                 (--no-config5 skips it)
+  config5_one_process
+                the same partitions from ONE process (rank 0) through
+                leveldb_crc32c_batch_multi over all N devices: PrismDB's shape,
+                8 partition threads of one process (db/db_impl.h:359,
+                util/env_posix.cc:850-890); one RCCL clique of N devices
+                (ncclCommInitAll), results gathered to device 0 over xGMI
+                (--no-multi skips it)
 """
 from __future__ import annotations
 
@@ -34,6 +45,8 @@ import ctypes
 import glob
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -62,6 +75,11 @@ def parse():
     ap.add_argument("--no-config5", action="store_true", help="skip the config-5 partition leg")
     ap.add_argument("--c5-spans", type=int, default=2_400_000, help="config-5 spans per partition (GPU)")
     ap.add_argument("--c5-steps", type=int, default=5)
+    ap.add_argument("--c5-files-per-call", type=int, default=7,
+                    help="config-5 compaction leg: SST files per leveldb_crc32c_batch call")
+    ap.add_argument("--no-multi", action="store_true", help="skip the one-process batch_multi leg")
+    ap.add_argument("--cpu-all-blocks", type=int, default=1 << 20,
+                    help="cpu_baseline all-cores figure: blocks (config 1: 1 Mi x 4 KiB)")
     return ap.parse_args()
 
 
@@ -101,9 +119,12 @@ def cpu_model() -> str:
     return "unknown"
 
 
-def cpu_baseline_leg(args, gpu_out) -> dict | None:
+def cpu_baseline_leg(args, gpu_out, dev_buf) -> dict | None:
     """Reference crc32c::Value timed on the host cores over the first
-    cpu_sample_blocks blocks of rank 0's shard; results compared with the GPU."""
+    cpu_sample_blocks blocks of rank 0's shard (regenerated on the host by the
+    oracle's splitmix64 fill); results compared with the GPU.  Plus the
+    config-1 figure: 1 Mi x 4 KiB on every core of the affinity
+    set, over the device's own bytes copied to the host."""
     import numpy as np
 
     ref_so = os.path.join(ROOT, "oracle", "_ref", "libref_crc32c.so")
@@ -125,8 +146,8 @@ def cpu_baseline_leg(args, gpu_out) -> dict | None:
                                                ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
         accel = int(lib.ref_crc32c_accelerated())
 
-        def run(t, p):
-            return lib.ref_crc32c_time_blocks(host.ctypes.data, BLOCK, BLOCK, nblk, t, p, out.ctypes.data)
+        def run(t, p, arr=host, o=out, nb=nblk):
+            return lib.ref_crc32c_time_blocks(arr.ctypes.data, BLOCK, BLOCK, nb, t, p, o.ctypes.data)
     else:
         # oracle/_ref/ (the reference compiled from /root/reference, shipped
         # with the snapshot) is missing: time the C restatement instead, and
@@ -139,10 +160,10 @@ def cpu_baseline_leg(args, gpu_out) -> dict | None:
                                                   ctypes.c_size_t, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32]
         threads = 1
 
-        def run(t, p):
+        def run(t, p, arr=host, o=out, nb=nblk):
             t0 = time.perf_counter()
             for _ in range(p):
-                ora.oracle_crc32c_batch_fixed(host.ctypes.data, BLOCK, BLOCK, nblk, 0, out.ctypes.data, 0)
+                ora.oracle_crc32c_batch_fixed(arr.ctypes.data, BLOCK, BLOCK, nb, 0, o.ctypes.data, 0)
             return time.perf_counter() - t0
 
     t1 = run(1, 1)  # single-thread calibration pass
@@ -154,7 +175,7 @@ def cpu_baseline_leg(args, gpu_out) -> dict | None:
     g = gpu_out[:nblk].cpu().numpy().view(np.uint32)
     agree = int((g == out).sum())
     cpus = affinity()
-    return {
+    res = {
         "value": round(rate, 3), "unit": "GiB/s", "cores": threads, "kind": kind,
         "host_cores_total": os.cpu_count(),
         "affinity": {"count": len(cpus), "cpus": _ranges(cpus)},
@@ -169,6 +190,26 @@ def cpu_baseline_leg(args, gpu_out) -> dict | None:
         "cpu_model": cpu_model(),
         "agrees_with_gpu": f"{agree}/{nblk}",
     }
+    # config 1 as SURVEY 8(d) states it: 1 Mi x 4 KiB at all host cores (the
+    # affinity set), bytes from the device buffer (the same stream)
+    nall = min(args.cpu_all_blocks, args.nblocks)
+    if kind == "reference" and nall > 0:
+        big = dev_buf[:nall * BLOCK].cpu().numpy()
+        oall = np.empty(nall, dtype=np.uint32)
+        nthr = len(cpus)
+        t_one = max(t1 * nall / nblk / nthr, 1e-6)  # ~wall seconds of one pass on nthr threads
+        p_all = max(1, int(round(2.0 / t_one)))  # ~2 s of wall time
+        ta = run(nthr, p_all, big, oall, nall)
+        ga = gpu_out[:nall].cpu().numpy().view(np.uint32)
+        res["all_cores"] = {
+            "value": round(nall * BLOCK * p_all / ta / GIB, 3), "unit": "GiB/s", "threads": nthr,
+            "blocks": nall, "passes": p_all, "wall_s": round(ta, 3),
+            "sample": f"config 1: crc32c::Value over {nall} x 4096 B host-resident blocks on every core of the "
+                      f"affinity set ({nthr} threads; the box's CPU share for one GPU may be smaller)",
+            "agrees_with_gpu": f"{int((ga == oall).sum())}/{nall}",
+        }
+        del big
+    return res
 
 
 def load_pmc_traffic(nblocks: int):
@@ -292,21 +333,36 @@ def compaction_leg(torch, crc32c, dev, nfiles: int = 115) -> dict:
 C5_ND, C5_DATA, C5_STRIDE, C5_INDEX = 16811, 3988, 3992, 486977  # one 64 MiB SST
 
 
+def _c5_descriptors(nfiles: int):
+    """Descriptors of nfiles consecutive SST files of the config-5 layout
+    (file f at f * fbytes): offsets, lengths, type-byte positions."""
+    import numpy as np
+
+    fbytes = (C5_ND * C5_STRIDE + C5_INDEX + 4 + 255) & ~255
+    off1 = np.concatenate([np.arange(C5_ND, dtype=np.int64) * C5_STRIDE, [C5_ND * C5_STRIDE]])
+    len1 = np.concatenate([np.full(C5_ND, C5_DATA, dtype=np.int64), [C5_INDEX]])
+    off = (np.arange(nfiles, dtype=np.int64)[:, None] * fbytes + off1[None, :]).reshape(-1)
+    lens = np.tile(len1, nfiles)
+    return fbytes, off, lens, off + lens - 1
+
+
 def config5_leg(args, torch, dist, crc32c, dev, rank, world) -> dict:
     """BASELINE configs[4] (scripts/config_test_100gb.yml): 8 partitions, ~19.3 M
     block spans, partition p on GPU p -- ~2.4 M spans per GPU, here as the SST
     files that partition's compactions write: nfiles x (16 811 data spans of
     contents||type = 3988 B at stride 3992 + one 486 977-B index span), device-
-    resident.  One step = every file of the partition through one
-    leveldb_crc32c_batch call each (the granularity PrismDB calls at:
-    TableBuilder::Finish seals a file, table/table_builder.cc:185-261; a
-    compaction verifies its inputs block by block, table/format.cc:91-102),
-    then (N > 1) one RCCL gather of the partition's 4-byte results to rank 0.
+    resident.  One step = every file of the partition, then (N > 1) one RCCL
+    gather of the partition's 4-byte results to rank 0.  Two granularities:
+      per file        one leveldb_crc32c_batch per file -- TableBuilder::Finish
+                      seals a file (table/table_builder.cc:185-261), ReadBlock
+                      verifies a block at a time (table/format.cc:91-102)
+      per compaction  one call per --c5-files-per-call files: a compaction's
+                      input set verified together (db/version_set.cc:1265-1300
+                      opens them as one merging iterator), or its output files
+                      sealed together
     Seal = MASK | WRITE_TRAILER (trailers written in place), verify = the
-    mismatch vector; consecutive file calls carry PRISMDB_CRC32C_UNORDERED
-    (the files are disjoint), and the seal is also timed in stream order.
-    GiB/s of span bytes, whole job (all ranks), max-over-ranks timing
-    between barriers.  Checks: verify after seal flags nothing
+    mismatch vector.  GiB/s of span bytes, whole job (all ranks), max-over-
+    ranks timing between barriers.  Checks: verify after seal flags nothing
     and returns the unmasked seal results; 256 spans of file 0 against the
     host leveldb_crc32c_value; the gathered digests."""
     import numpy as np
@@ -315,16 +371,15 @@ def config5_leg(args, torch, dist, crc32c, dev, rank, world) -> dict:
 
     spf = C5_ND + 1
     nfiles = -(-args.c5_spans // spf)
-    fbytes = (C5_ND * C5_STRIDE + C5_INDEX + 4 + 255) & ~255
     span_bytes = C5_ND * C5_DATA + C5_INDEX
+    fbytes, off_all, len_all, typ = _c5_descriptors(nfiles)
+    off1, len1 = off_all[:spf], len_all[:spf]
     buf = torch.empty(nfiles * fbytes, dtype=torch.uint8, device=dev)
     crc32c.fill_synthetic(buf, SEED ^ 0xC5C5, byte_offset=rank * nfiles * fbytes)
-    off1 = np.concatenate([np.arange(C5_ND, dtype=np.int64) * C5_STRIDE, [C5_ND * C5_STRIDE]])
-    len1 = np.concatenate([np.full(C5_ND, C5_DATA, dtype=np.int64), [C5_INDEX]])
-    typ = (np.arange(nfiles, dtype=np.int64)[:, None] * fbytes + (off1 + len1 - 1)[None, :]).reshape(-1)
     buf[torch.from_numpy(typ).to(dev)] = 0  # type byte kNoCompression
-    d_off = torch.from_numpy(off1).to(dev)
-    d_len = torch.from_numpy(len1.astype(np.int32)).to(dev)
+    kpc = max(1, min(args.c5_files_per_call, nfiles))
+    d_off = torch.from_numpy(off_all[:kpc * spf].copy()).to(dev)  # kpc consecutive files from file 0
+    d_len = torch.from_numpy(len_all[:kpc * spf].astype(np.int32)).to(dev)
     n = nfiles * spf
     out = torch.empty(n, dtype=torch.int32, device=dev)
     raw = torch.empty(n, dtype=torch.int32, device=dev)
@@ -334,11 +389,12 @@ def config5_leg(args, torch, dist, crc32c, dev, rank, world) -> dict:
     sp = int(stream.cuda_stream)
     base, op, lp = buf.data_ptr(), d_off.data_ptr(), d_len.data_ptr()
 
-    def run(verify, unordered):
+    def run(verify, k):
         o = raw.data_ptr() if verify else out.data_ptr()
-        fl = (0 if verify else 0x3) | (0x8 if unordered else 0)  # seal: MASK | WRITE_TRAILER; 0x8: UNORDERED
-        for f in range(nfiles):
-            rc = L.leveldb_crc32c_batch(base + f * fbytes, op, lp, None, spf, o + 4 * f * spf,
+        fl = 0 if verify else 0x3  # seal: MASK | WRITE_TRAILER
+        for f in range(0, nfiles, k):
+            m = min(k, nfiles - f) * spf
+            rc = L.leveldb_crc32c_batch(base + f * fbytes, op, lp, None, m, o + 4 * f * spf,
                                         (mm.data_ptr() + f * spf) if verify else None, fl, sp)
             if rc != 0:
                 raise RuntimeError(f"leveldb_crc32c_batch: {L.leveldb_crc32c_last_error().decode()}")
@@ -346,12 +402,12 @@ def config5_leg(args, torch, dist, crc32c, dev, rank, world) -> dict:
     shard = ShardedBatch(nblocks_per_rank=n, block_bytes=0, rank=rank, world=world, device=dev, slots=1) \
         if world > 1 else None
 
-    def leg(verify, unordered=True):
+    def leg(verify, k):
         res = out if not verify else raw
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
               for _ in range(args.c5_steps)]
         for _ in range(2):
-            run(verify, unordered)
+            run(verify, k)
             if shard:
                 shard.gather_async(res, 0).wait()
         torch.cuda.synchronize()
@@ -361,7 +417,7 @@ def config5_leg(args, torch, dist, crc32c, dev, rank, world) -> dict:
         t0 = time.perf_counter()
         for i in range(args.c5_steps):
             ev[i][0].record(stream)
-            run(verify, unordered)
+            run(verify, k)
             ev[i][1].record(stream)
             if shard:
                 shard.gather_async(res, 0).wait()
@@ -375,17 +431,22 @@ def config5_leg(args, torch, dist, crc32c, dev, rank, world) -> dict:
         if world > 1:
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el, kern = float(t[0]), float(t[1])
+        calls = -(-nfiles // k)
         d = {"value": round(world * nfiles * span_bytes * args.c5_steps / el / GIB, 2), "unit": "GiB/s",
              "ms_per_step": round(el * 1e3 / args.c5_steps, 3),
              "batch_ms_per_step_max_rank": round(kern, 3),
-             "us_per_file_call": round(kern * 1e3 / nfiles, 2)}
+             "files_per_call": k, "calls_per_step": calls,
+             "us_per_call": round(kern * 1e3 / calls, 2),
+             "us_per_file": round(kern * 1e3 / nfiles, 2),
+             "roofline_frac_per_gpu": round(nfiles * (span_bytes + 4 * spf) / (kern / 1e3) / 1e9 / HBM_PEAK_GBS, 4)}
         if shard:
             d["gather_check"] = shard.check_gathered(res, 0)
         return d
 
-    seal = leg(False)
-    verify = leg(True)
-    seal_ordered = leg(False, unordered=False)
+    seal = leg(False, 1)
+    verify = leg(True, 1)
+    seal_c = leg(False, kpc)
+    verify_c = leg(True, kpc)
     torch.cuda.synchronize()
     bad = int(mm.sum().item())
     unmasked = (out.to(torch.int64) & 0xFFFFFFFF) - 0xA282EAD8
@@ -400,33 +461,136 @@ def config5_leg(args, torch, dist, crc32c, dev, rank, world) -> dict:
     return {
         "workload": (f"config5: partition {rank} of {world} on GPU {rank}: {nfiles} SST files x ({C5_ND} x "
                      f"{C5_DATA} B @ {C5_STRIDE} + 1 x {C5_INDEX} B) = {n} spans per GPU, one "
-                     "leveldb_crc32c_batch per file" + (", RCCL gather of the results to rank 0" if world > 1 else "")),
+                     f"leveldb_crc32c_batch per file (seal, verify) or per {kpc} files (seal_compaction, "
+                     "verify_compaction)" + (", RCCL gather of the results to rank 0" if world > 1 else "")),
         "files_per_gpu": nfiles, "spans_per_gpu": n, "span_bytes_per_gpu": nfiles * span_bytes,
         "steps": args.c5_steps, "scaling": "weak",
-        "seal": seal, "verify": verify, "seal_ordered": seal_ordered,
-        "note": ("seal / verify: consecutive file calls flagged PRISMDB_CRC32C_UNORDERED (the files are disjoint: "
-                 "every other launch may overlap its predecessor); seal_ordered: the same calls in stream order"),
+        "seal": seal, "verify": verify, "seal_compaction": seal_c, "verify_compaction": verify_c,
         "checks": {"verify_after_seal_mismatches": bad, "verify_equals_unmasked_seal": same,
                    "host_value_256_spans_file0": host_ok},
     }
 
 
+def multi_leg(args, torch, crc32c, ndev: int) -> dict:
+    """Config 5 from ONE process, PrismDB's own shape (its 8 partitions are
+    threads of one process, db/db_impl.h:359, util/env_posix.cc:850-890):
+    partition p = the config-5 SST files of partition p, resident on device p;
+    one leveldb_crc32c_batch_multi call per step seals every partition on its
+    own device and gathers the 4-byte results to device 0 over RCCL (one
+    clique of ndev devices, ncclCommInitAll).  Timed next to the same
+    per-device batches issued without the gather.  Checks: the gathered
+    vector equals the per-device results concatenated; a verify pass over
+    the sealed partitions flags nothing."""
+    import numpy as np
+
+    spf = C5_ND + 1
+    nfiles = -(-args.c5_spans // spf)
+    span_bytes = C5_ND * C5_DATA + C5_INDEX
+    fbytes, off_all, len_all, typ = _c5_descriptors(nfiles)
+    n = nfiles * spf
+    parts, streams = [], []
+    for p in range(ndev):
+        d = torch.device("cuda", p)
+        with torch.cuda.device(d):
+            crc32c.device_init(p)
+            buf = torch.empty(nfiles * fbytes, dtype=torch.uint8, device=d)
+            crc32c.fill_synthetic(buf, SEED ^ 0xC5C5, byte_offset=p * nfiles * fbytes)
+            buf[torch.from_numpy(typ).to(d)] = 0
+            parts.append((buf, torch.from_numpy(off_all).to(d), torch.from_numpy(len_all.astype(np.int32)).to(d)))
+            streams.append(torch.cuda.current_stream(d))
+    root = torch.device("cuda", 0)
+    out = torch.empty(ndev * n, dtype=torch.int32, device=root)
+    mm = torch.empty(ndev * n, dtype=torch.uint8, device=root)
+    sep = [torch.empty(n, dtype=torch.int32, device=torch.device("cuda", p)) for p in range(ndev)]
+
+    def sync_all():
+        for p in range(ndev):
+            torch.cuda.synchronize(p)
+
+    def gathered():
+        crc32c.batch_multi(parts, mask=True, trailer=True, out=out, streams=streams, check_bounds=False)
+
+    def separate():
+        for p in range(ndev):
+            with torch.cuda.device(p):
+                crc32c.batch(*parts[p], mask=True, trailer=True, out=sep[p], stream=streams[p], check_bounds=False)
+
+    res = {"devices": ndev, "clique": ndev, "files_per_device": nfiles, "spans_per_device": n,
+           "steps": args.c5_steps, "call": "one leveldb_crc32c_batch_multi per step: every partition sealed "
+           "(MASK | WRITE_TRAILER) on its device, results gathered to device 0"}
+    for name, fn in (("with_gather", gathered), ("without_gather", separate)):
+        fn()
+        sync_all()
+        t0 = time.perf_counter()
+        for _ in range(args.c5_steps):
+            fn()
+        sync_all()
+        el = time.perf_counter() - t0
+        res[name] = {"value": round(ndev * nfiles * span_bytes * args.c5_steps / el / GIB, 2), "unit": "GiB/s",
+                     "ms_per_step": round(el * 1e3 / args.c5_steps, 3)}
+    want = torch.cat([t.to(root) for t in sep])
+    res["gather_check"] = {"gathered_equals_per_device": bool(torch.equal(out, want)), "entries": int(out.numel())}
+    crc32c.batch_multi(parts, verify=True, out=out, mismatch=mm, streams=streams, check_bounds=False)
+    sync_all()
+    res["verify_after_seal_mismatches"] = int(mm.sum().item())
+    del parts, sep, out, mm
+    for p in range(ndev):
+        with torch.cuda.device(p):
+            torch.cuda.empty_cache()
+    return res
+
+
+def free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def spawn_ranks(args) -> int:
+    """--gpus N > 1 without a launcher: start N ranks under
+    torch.distributed.run from this process, which never touches the GPU
+    (no HIP call before the children exist, no exec after one), and return
+    their status.  The ranks' rank 0 prints the JSON line."""
+    import torch
+
+    have = torch.cuda.device_count()  # counts devices without initialising HIP on this image
+    if have and args.gpus > have:
+        print(f"error: --gpus {args.gpus} but only {have} devices are visible", file=sys.stderr)
+        return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    print(f"bench: no WORLD_SIZE; launching {args.gpus} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    return subprocess.call(cmd, env=env)
+
+
 def main() -> int:
     args = parse()
-    import torch
-    import torch.distributed as dist
-
+    # The launch mode is settled before anything touches the GPU.
+    if os.environ.get("WORLD_SIZE") is None and args.gpus > 1:
+        return spawn_ranks(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        if rank == 0:
-            print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
+        print(f"error: --gpus {args.gpus} but WORLD_SIZE {world}: refusing to measure another world size",
+              file=sys.stderr)
+        return 2
+    if os.environ.get("PRISMDB_BENCH_DRYRUN"):  # tests: the launch alone, no GPU
+        print(json.dumps({"dryrun": True, "rank": rank, "world": world, "local_rank": local}), flush=True)
+        return 0
+    import torch
+    import torch.distributed as dist
+
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    cpu_group = None
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl", device_id=dev)
+        # ranks that wait while rank 0 drives every device wait here, on the
+        # host (an RCCL barrier would leave a spinning kernel on their device)
+        cpu_group = dist.new_group(backend="gloo")
 
     from prismdb_amd import crc32c
     from prismdb_amd.dist import ShardedBatch
@@ -500,13 +664,28 @@ def main() -> int:
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline_leg(args, outs[(args.steps - 1) % 2])
+        cpu = cpu_baseline_leg(args, outs[(args.steps - 1) % 2], buf)
     e2e = e2e_leg(args, torch, crc32c, dev) if (args.e2e and rank == 0 and world == 1) else None
+    del buf  # the config-2 blocks; the results stay for the checks above
+    torch.cuda.empty_cache()
     c5 = None
     if not args.no_config5:
-        del buf  # the config-2 blocks; the results stay for the checks above
-        torch.cuda.empty_cache()
         c5 = config5_leg(args, torch, dist, crc32c, dev, rank, world)
+    multi = None
+    if not args.no_multi:
+        # rank 0 alone drives all `world` devices; the others free their
+        # memory and wait on the host
+        del outs
+        torch.cuda.empty_cache()
+        if world > 1:
+            dist.barrier(group=cpu_group)
+        if rank == 0:
+            try:
+                multi = multi_leg(args, torch, crc32c, world)
+            except Exception as e:  # reported in the line; the headline stands on its own
+                multi = {"devices": world, "error": f"{type(e).__name__}: {e}"}
+        if world > 1:
+            dist.barrier(group=cpu_group)
 
     if rank == 0:
         pmc = load_pmc_traffic(nblk)
@@ -556,6 +735,8 @@ def main() -> int:
             line["e2e_host_resident"] = e2e
         if c5 is not None:
             line["config5_partitions"] = c5
+        if multi is not None:
+            line["config5_one_process"] = multi
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()

@@ -52,14 +52,11 @@ extern "C" {
  * Mask(Extend(type_crc[t], payload)) == Mask(Value(type||payload));
  * db/log_reader.cc:231-245 checks Value(header + 6, 1 + length)). */
 #define PRISMDB_CRC32C_LOG_HEADER 0x4u
-/* leveldb_crc32c_batch (batch_fixed and batch_multi accept and ignore it,
- * batch_host rejects it): this batch
- * may start before the batch issued just before it on the same stream has
- * finished -- the caller promises the two touch disjoint bytes (e.g. two SST
- * files a compaction seals one after the other: table/table_builder.cc:206-261
- * per file).  Consecutive UNORDERED batches alternate with ordered launches,
- * so at most two batches of a stream are in flight.  Everything else keeps
- * stream order: a later batch without the flag waits for both. */
+/* Accepted and ignored by leveldb_crc32c_batch, batch_fixed and batch_multi
+ * (batch_host rejects it); kept so that callers built against round 3's
+ * header still link and run.  Every batch runs in stream order: the
+ * any-order launch it used to request is not supported on gfx9
+ * (hip/hip_ext.h, hipExtAnyOrderLaunch) and measured slower where it ran. */
 #define PRISMDB_CRC32C_UNORDERED 0x8u
 
 /* error codes */

@@ -138,9 +138,8 @@ def batch(buf, off, lens, init=None, *, mask: bool = False, verify: bool = False
     that reuse descriptors they have already checked pass False and stay
     asynchronous.
 
-    unordered: PRISMDB_CRC32C_UNORDERED -- this batch may overlap the batch
-    issued just before it on the stream (the caller promises they touch
-    disjoint bytes, e.g. consecutive SST files of a compaction)."""
+    unordered: PRISMDB_CRC32C_UNORDERED, accepted and ignored (every batch
+    runs in stream order; see include/prismdb_crc32c.h)."""
     if trailer and verify:
         raise ValueError("trailer and verify are exclusive")
     torch = _torch()
@@ -231,6 +230,13 @@ def batch_multi(parts, *, mask: bool = False, verify: bool = False, trailer: boo
         out = torch.empty(total, dtype=torch.int32, device=root)
     if verify and mismatch is None:
         mismatch = torch.empty(total, dtype=torch.uint8, device=root)
+    # the C side writes n[0] + ... + n[ndev-1] entries at out / mismatch on the root device
+    for name, t, dt in (("out", out, torch.int32), ("mismatch", mismatch if verify else None, torch.uint8)):
+        if t is None:
+            continue
+        if t.dtype != dt or t.device != root or not t.is_contiguous() or t.numel() < total:
+            raise ValueError(f"batch_multi: {name} must be a contiguous {dt} tensor of >= {total} entries "
+                             f"on {root} (got {t.dtype}, {t.numel()} on {t.device})")
     P = ctypes.c_void_p * ndev
     c_dev = (ctypes.c_int * ndev)(*devs)
     c_base = P(*bases)

@@ -232,7 +232,6 @@ struct Workspace {
   // calls alternate between two slots; the planner path marks done[gen & 1]):
   // waiting for both covers everything that used the workspace.
   hipEvent_t done[2] = {nullptr, nullptr};
-  bool prev_any = false;  // the last one-launch call was an any-order launch
   void* mem = nullptr;
   char* grow = nullptr;
   size_t cap_rec = 0;
@@ -294,8 +293,13 @@ size_t SliceCap(size_t n, uint32_t streams) {
 constexpr uint64_t kCapSeg = 1u << 20;   // 1 Mi segments = 32 GiB of long spans per call
 constexpr uint32_t kCapLong = 1u << 18;
 
-Workspace* FindWorkspace(hipStream_t s, int& rc) {
+WorkspaceCache& ThreadWorkspaces() {
   thread_local WorkspaceCache cache;
+  return cache;
+}
+
+Workspace* FindWorkspace(hipStream_t s, int& rc) {
+  WorkspaceCache& cache = ThreadWorkspaces();
   int device = 0;
   hipError_t e = hipGetDevice(&device);
   if (e != hipSuccess) {
@@ -398,8 +402,8 @@ int PlannerWorkspace(Workspace& w, hipStream_t s, size_t nspans, uint32_t stream
 }
 
 // The one-launch path's workspace: four claim words (call g uses word g % 4
-// and zeroes word (g + 2) % 4 for the call after next; at most two calls of a
-// stream are in flight, PRISMDB_CRC32C_UNORDERED), the usage counters, and
+// and zeroes word (g + 2) % 4 for the call after next; calls of a stream run
+// in stream order, so the word a call zeroes is idle), the usage counters, and
 // two slots (call parity) of: the ticket map (32-B entries of four words
 // tagged with the call's gen), the tagged partial registers and the per-span
 // ticket counters (zero between calls: a span's combiner resets its own).
@@ -415,13 +419,13 @@ int DirectWorkspace(Workspace& w, hipStream_t s, prismdb::dev::DirectWs* out) {
   }
   // Generations: the words a call writes carry gen's low 16 bits (its tag),
   // so words of earlier calls never match.  At the wrap (2^16 calls) the
-  // workspace is zeroed again (an ordered command: behind both slots' last
-  // calls) and the count restarts.
+  // workspace is zeroed again (a fill kernel in stream order: behind both
+  // slots' last calls, ahead of the next one -- every one-launch call is an
+  // ordered launch) and the count restarts.
   if ((++w.gen & d::kTagMask) == 0) {
     hipError_t e = hipMemsetAsync(w.direct, 0, bytes, s);
     if (e != hipSuccess) return FailHip(e, "ticket workspace memset");
     w.gen = 1;
-    w.prev_any = false;
   }
   char* p = w.direct;
   out->word = reinterpret_cast<unsigned long long*>(p + 8 * (w.gen & 3u));
@@ -447,7 +451,9 @@ enum Route { kRouteAuto = 0, kRouteDirect = 1, kRoutePlanner = 2 };
 // list in front for log-record batches.
 int RunBatch(DeviceCtx& ctx, const SpanBatch& base_args, bool desc, bool verify, hipStream_t s, int route) {
   SpanBatch a = base_args;
-  const bool unordered = (a.flags & PRISMDB_CRC32C_UNORDERED) != 0;  // host-side only
+  // PRISMDB_CRC32C_UNORDERED is accepted and has no effect: every launch is
+  // in stream order (an any-order launch is not supported on gfx9, and it
+  // measured slower where it ran: 25.9 against 24.9 us per SST file)
   a.flags &= ~PRISMDB_CRC32C_UNORDERED;
   a.tabs = ctx.tabs;
   a.role = prismdb::dev::kRoleSpans;
@@ -475,10 +481,7 @@ int RunBatch(DeviceCtx& ctx, const SpanBatch& base_args, bool desc, bool verify,
     hipStream_t s;
     bool by_launch = false;
     ~MarkDone() {
-      if (!by_launch) {
-        (void)hipEventRecord(w->done[w->gen & 1u], s);
-        w->prev_any = false;
-      }
+      if (!by_launch) (void)hipEventRecord(w->done[w->gen & 1u], s);
     }
   } mark{w, s};
   const bool direct = desc && (route == kRouteDirect ||
@@ -491,10 +494,7 @@ int RunBatch(DeviceCtx& ctx, const SpanBatch& base_args, bool desc, bool verify,
     t_last_stats = d.stats;
     t_last_stream = s;
     mark.by_launch = true;
-    // PRISMDB_CRC32C_UNORDERED: every other call may overlap its predecessor
-    const bool any = unordered && !w->prev_any;
-    w->prev_any = any;
-    hipError_t e = prismdb::dev::launch_direct(a, verify, ctx.cus, d, s, w->done[w->gen & 1u], any);
+    hipError_t e = prismdb::dev::launch_direct(a, verify, ctx.cus, d, s, w->done[w->gen & 1u]);
     return e == hipSuccess ? 0 : FailHip(e, "direct kernel launch");
   }
   // The span kernel indexes records with 32 bits: cut larger batches.
@@ -690,6 +690,22 @@ uint32_t prismdb_crc32c_direct_tickets(uint32_t cap) {
   return g_direct_cap.exchange(cap, std::memory_order_relaxed);
 }
 uint32_t prismdb_crc32c_direct_debug(uint32_t flags) { return g_direct_dbg.exchange(flags, std::memory_order_relaxed); }
+
+// the call count of the calling thread's workspace for (current device,
+// stream): the next one-launch call there takes gen + 1 (its tag: the low 16
+// bits; gen + 1 == 0 mod 2^16 zeroes the workspace first).  Lets a test cross
+// the tag wrap in a few calls.  0, or -1 if the thread has no such workspace.
+int prismdb_crc32c_direct_set_gen(void* stream, uint32_t gen) {
+  int device = 0;
+  if (hipGetDevice(&device) != hipSuccess) return -1;
+  for (Workspace& w : ThreadWorkspaces().lru) {
+    if (w.device == device && w.stream == static_cast<hipStream_t>(stream) && w.direct != nullptr) {
+      w.gen = gen;
+      return 0;
+    }
+  }
+  return -1;
+}
 
 // the cumulative one-launch counters of the workspace of the calling thread's
 // last one-launch batch {tickets adopted, spans folded whole, tickets claimed

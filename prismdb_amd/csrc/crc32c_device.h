@@ -186,11 +186,9 @@ hipError_t launch_lane(const SpanBatch& a, bool verify, int grid, const SplitWs&
 constexpr int kListThreads = 1024;  // crc32c_long_list_kernel block: one atomic per 16 runs
 // `done` is recorded when the kernel completes (the launch's own completion
 // signal: a separate hipEventRecord marker cost ~5.7 us between back-to-back
-// calls).
-// any_order: the launch may start before the stream's previous kernel ends
-// (hipExtAnyOrderLaunch; PRISMDB_CRC32C_UNORDERED batches).
+// calls).  Always an ordered launch.
 hipError_t launch_direct(const SpanBatch& a, bool verify, int grid, const DirectWs& d, hipStream_t s,
-                         hipEvent_t done, bool any_order);
+                         hipEvent_t done);
 hipError_t launch_scatter(const SpanBatch& a, const SplitWs& ws, const uint32_t* qout, const uint8_t* qmm,
                           hipStream_t s);
 

@@ -807,12 +807,11 @@ __global__ __launch_bounds__(kDirectThreads) void crc32c_direct_kernel(SpanBatch
 }
 
 hipError_t launch_direct(const SpanBatch& a, bool verify, int grid, const DirectWs& d, hipStream_t s,
-                         hipEvent_t done, bool any_order) {
-  const uint32_t fl = any_order ? (uint32_t)hipExtAnyOrderLaunch : 0u;
+                         hipEvent_t done) {
   if (verify)
-    hipExtLaunchKernelGGL(crc32c_direct_kernel<true>, dim3(grid), dim3(kDirectThreads), 0, s, nullptr, done, fl, a, d);
+    hipExtLaunchKernelGGL(crc32c_direct_kernel<true>, dim3(grid), dim3(kDirectThreads), 0, s, nullptr, done, 0u, a, d);
   else
-    hipExtLaunchKernelGGL(crc32c_direct_kernel<false>, dim3(grid), dim3(kDirectThreads), 0, s, nullptr, done, fl, a, d);
+    hipExtLaunchKernelGGL(crc32c_direct_kernel<false>, dim3(grid), dim3(kDirectThreads), 0, s, nullptr, done, 0u, a, d);
   return hipGetLastError();
 }
 

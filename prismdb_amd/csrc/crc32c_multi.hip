@@ -10,13 +10,15 @@
 //
 // A clique (the RCCL communicators of one device list, ncclCommInitAll) is
 // created on the first call for that list and kept; its calls are serialized
-// (RCCL communicators are not for concurrent use) on one internal stream per
-// device, which waits for the caller's stream first and which the caller's
-// stream waits for afterwards.  Partition 0 writes its results straight into
+// (RCCL communicators are not for concurrent use: calls with the same device
+// list queue on the clique's mutex) on one internal stream per device, which
+// waits for the caller's stream first and which the caller's stream waits for
+// afterwards -- on every return, errors included.  Partition 0 writes its results straight into
 // out0; the others go through per-device scratch, grown stream-ordered.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <atomic>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -59,6 +61,7 @@ struct Clique {
 // torn down inside exit(), where the runtime may be going away).
 std::mutex g_mu;
 std::vector<Clique*> g_cliques;
+std::atomic<int> g_fail_after{-1};  // test hook: prismdb_crc32c_multi_fail_after
 
 int GetClique(int ndev, const int* devices, Clique** out) {
   std::lock_guard<std::mutex> lk(g_mu);
@@ -132,18 +135,35 @@ int leveldb_crc32c_batch_multi(int ndev, const int* devices, const void* const* 
   int rc = GetClique(ndev, devices, &c);
   if (rc != 0) return rc;
   std::lock_guard<std::mutex> lk(c->mu);
-  auto restore = [&](int code) {
+  // Once the first command is on a clique stream, every return goes through
+  // here: the caller's streams wait for everything the call enqueued (its
+  // batches, scratch growth, the gather), so a caller that frees or reuses
+  // its buffers after an error never races the clique's work.  If a hand-off
+  // itself fails, the clique's streams are drained instead.
+  int enqueued = 0;  // clique streams [0, enqueued) may hold work of this call
+  auto finish = [&](int code) {
+    for (int p = 0; p < enqueued; ++p) {
+      hipError_t h = hipSetDevice(devices[p]);
+      hipStream_t user = streams != nullptr ? static_cast<hipStream_t>(streams[p]) : nullptr;
+      if (h == hipSuccess) h = hipEventRecord(c->events[p], c->streams[p]);
+      if (h == hipSuccess) h = hipStreamWaitEvent(user, c->events[p], 0);
+      if (h != hipSuccess) {
+        (void)hipStreamSynchronize(c->streams[p]);
+        if (code == 0) code = HipFail(h, "hand-off to the caller's stream");
+      }
+    }
     (void)hipSetDevice(cur);
     return code;
   };
   // the clique's streams start after the caller's, and partitions > 0 get
   // scratch for their results
   for (int p = 0; p < ndev; ++p) {
-    if ((e = hipSetDevice(devices[p])) != hipSuccess) return restore(HipFail(e, "hipSetDevice"));
+    if ((e = hipSetDevice(devices[p])) != hipSuccess) return finish(HipFail(e, "hipSetDevice"));
     hipStream_t user = streams != nullptr ? static_cast<hipStream_t>(streams[p]) : nullptr;
-    if ((e = hipEventRecord(c->events[p], user)) != hipSuccess) return restore(HipFail(e, "hipEventRecord"));
+    if ((e = hipEventRecord(c->events[p], user)) != hipSuccess) return finish(HipFail(e, "hipEventRecord"));
     if ((e = hipStreamWaitEvent(c->streams[p], c->events[p], 0)) != hipSuccess)
-      return restore(HipFail(e, "hipStreamWaitEvent"));
+      return finish(HipFail(e, "hipStreamWaitEvent"));
+    enqueued = p + 1;
     if (p > 0 && c->cap[p] < n[p]) {
       if (c->out[p] != nullptr) (void)hipFreeAsync(c->out[p], c->streams[p]);  // out and mm: one block
       c->out[p] = nullptr;
@@ -151,26 +171,30 @@ int leveldb_crc32c_batch_multi(int ndev, const int* devices, const void* const* 
       c->cap[p] = 0;
       const size_t cap = n[p] + n[p] / 4 + 1024;
       void* blk = nullptr;
-      if ((e = hipMallocAsync(&blk, cap * 5, c->streams[p])) != hipSuccess) return restore(HipFail(e, "scratch"));
+      if ((e = hipMallocAsync(&blk, cap * 5, c->streams[p])) != hipSuccess) return finish(HipFail(e, "scratch"));
       c->out[p] = static_cast<uint32_t*>(blk);
       c->mm[p] = reinterpret_cast<uint8_t*>(c->out[p] + cap);
       c->cap[p] = cap;
     }
   }
   // every partition's batch on its own device
+  const int fail_after = g_fail_after.load(std::memory_order_relaxed);
   for (int p = 0; p < ndev; ++p) {
-    if (n[p] == 0) continue;
-    if ((e = hipSetDevice(devices[p])) != hipSuccess) return restore(HipFail(e, "hipSetDevice"));
-    uint32_t* o = out0 == nullptr ? nullptr : (p == 0 ? out0 : c->out[p]);
-    uint8_t* m = mismatch0 == nullptr ? nullptr : (p == 0 ? mismatch0 : c->mm[p]);
-    rc = leveldb_crc32c_batch(dev_base[p], dev_off[p], dev_len[p], dev_init != nullptr ? dev_init[p] : nullptr, n[p],
-                              o, m, flags, c->streams[p]);
-    if (rc != 0) return restore(rc);
+    if (n[p] != 0) {
+      if ((e = hipSetDevice(devices[p])) != hipSuccess) return finish(HipFail(e, "hipSetDevice"));
+      uint32_t* o = out0 == nullptr ? nullptr : (p == 0 ? out0 : c->out[p]);
+      uint8_t* m = mismatch0 == nullptr ? nullptr : (p == 0 ? mismatch0 : c->mm[p]);
+      rc = leveldb_crc32c_batch(dev_base[p], dev_off[p], dev_len[p], dev_init != nullptr ? dev_init[p] : nullptr,
+                                n[p], o, m, flags, c->streams[p]);
+      if (rc != 0) return finish(rc);
+    }
+    if (p == fail_after)
+      return finish(MultiFail(PRISMDB_CRC32C_EDEVICE, "batch_multi: injected failure (test hook)"));
   }
   // the gather to devices[0]: partition p's results at offset n[0] + ... + n[p-1]
   if (ndev > 1) {
     ncclResult_t r = ncclGroupStart();
-    if (r != ncclSuccess) return restore(NcclFail(r, "ncclGroupStart"));
+    if (r != ncclSuccess) return finish(NcclFail(r, "ncclGroupStart"));
     size_t at = n[0];
     for (int p = 1; p < ndev && r == ncclSuccess; ++p) {
       if (n[p] == 0) continue;
@@ -185,17 +209,15 @@ int leveldb_crc32c_batch_multi(int ndev, const int* devices, const void* const* 
       at += n[p];
     }
     const ncclResult_t r2 = ncclGroupEnd();
-    if (r != ncclSuccess) return restore(NcclFail(r, "ncclSend/ncclRecv"));
-    if (r2 != ncclSuccess) return restore(NcclFail(r2, "ncclGroupEnd"));
+    if (r != ncclSuccess) return finish(NcclFail(r, "ncclSend/ncclRecv"));
+    if (r2 != ncclSuccess) return finish(NcclFail(r2, "ncclGroupEnd"));
   }
   // the caller's streams resume after the clique's work
-  for (int p = 0; p < ndev; ++p) {
-    if ((e = hipSetDevice(devices[p])) != hipSuccess) return restore(HipFail(e, "hipSetDevice"));
-    hipStream_t user = streams != nullptr ? static_cast<hipStream_t>(streams[p]) : nullptr;
-    if ((e = hipEventRecord(c->events[p], c->streams[p])) != hipSuccess) return restore(HipFail(e, "hipEventRecord"));
-    if ((e = hipStreamWaitEvent(user, c->events[p], 0)) != hipSuccess) return restore(HipFail(e, "hipStreamWaitEvent"));
-  }
-  return restore(0);
+  return finish(0);
 }
+
+// Test hook (not in the public header): fail every call right after
+// partition p's batch is enqueued (-1: off); returns the previous value.
+int prismdb_crc32c_multi_fail_after(int p) { return g_fail_after.exchange(p < 0 ? -1 : p); }
 
 }  // extern "C"

@@ -546,13 +546,61 @@ def test_thread_churn_device_memory_flat(dev, oracle, native):
     assert free0 - free1 < 256 << 20, (free0 - free1) / 2**20
 
 
+def test_unordered_first_call_and_tag_wrap(dev, oracle, native):
+    """PRISMDB_CRC32C_UNORDERED (accepted, no effect) as the FIRST call on a
+    fresh stream -- right behind the ticket workspace's zero-fill -- on SST
+    files whose index span is cut into tickets; then the workspace's call
+    count is set just below the 16-bit tag wrap (test hook), and five more
+    ticketed calls cross it (the wrap zeroes the workspace again between
+    two calls).  Every result, verify flag and trailer against the oracle."""
+    import torch
+    from prismdb_amd import crc32c
+
+    nf = 2
+    host, off, lens, raw, masked = _sst_file(oracle, 0x5EED00DC, files=nf)
+    per = len(off) // nf
+    s = torch.cuda.Stream(dev)
+    with torch.cuda.stream(s):
+        buf = torch.from_numpy(host).to(dev)
+        d_off = torch.from_numpy(off.astype(np.int64)).to(dev)
+        d_len = torch.from_numpy(lens.view(np.int32)).to(dev)
+        outs = torch.full((7, per), 7, dtype=torch.int32, device=dev)
+        mms = torch.full((7, per), 7, dtype=torch.uint8, device=dev)
+
+    def call(i, f, verify):
+        sl = slice(f * per, (f + 1) * per)
+        if verify:
+            crc32c.batch(buf, d_off[sl], d_len[sl], verify=True, out=outs[i], mismatch=mms[i], check_bounds=False,
+                         unordered=True, stream=s)
+        else:
+            crc32c.batch(buf, d_off[sl], d_len[sl], mask=True, trailer=True, out=outs[i], check_bounds=False,
+                         unordered=True, stream=s)
+
+    call(0, 0, False)  # the stream's first call: workspace allocated and zeroed, then this launch
+    s.synchronize()
+    sp = ctypes.c_void_p(int(s.cuda_stream))
+    assert native.prismdb_crc32c_direct_set_gen(sp, 0xFFFD) == 0
+    plan = [(1, 1, True), (2, 0, False), (3, 1, False), (4, 0, True), (5, 1, True), (6, 0, True)]
+    for i, f, v in plan:  # tags 0xFFFE, 0xFFFF, wrap (zero-fill) -> 1, 2, 3, 4
+        call(i, f, v)
+    s.synchronize()
+    assert _last_split_rc(native) == -2
+    got = outs.cpu().numpy().view(np.uint32)
+    mm = mms.cpu().numpy()
+    for i, f, v in [(0, 0, False)] + plan:
+        want = (raw if v else masked)[f * per:(f + 1) * per]
+        np.testing.assert_array_equal(got[i], want, err_msg=f"call {i}")
+        if v:
+            assert not mm[i].any(), f"call {i}"
+    assert (buf.cpu().numpy() == host).all()
+
+
 def test_unordered_file_calls(dev, oracle, native):
-    """PRISMDB_CRC32C_UNORDERED: 24 SST files sealed one call each, back to
-    back (every other launch may overlap its predecessor: the files are
-    disjoint), then all verified the same way (each file's verify after its
-    seal: at most the call just before may overlap), then an ordered verify
-    right after an unordered reseal of the same file.  Every result, every
-    trailer and every verify flag against the oracle."""
+    """PRISMDB_CRC32C_UNORDERED (accepted and ignored: every launch is in
+    stream order): 24 SST files sealed one call each, back to back, then all
+    verified the same way, then a verify right after a flagged reseal of the
+    same file.  Every result, every trailer and every verify flag against the
+    oracle."""
     import torch
     from prismdb_amd import crc32c
 

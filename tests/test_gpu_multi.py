@@ -120,3 +120,55 @@ def test_multi_all_devices(devices, oracle):
     out, _ = crc32c.batch_multi(parts, mask=True)
     assert out.device.index == devices[0]
     np.testing.assert_array_equal(_u32(out), np.concatenate(want))
+
+
+def test_multi_failure_hands_streams_back(devices, oracle, native):
+    """An injected failure right after partition 0's batch is enqueued (test
+    hook prismdb_crc32c_multi_fail_after): the call raises, and the caller's
+    stream still waits for the clique's work -- a fill of `out` enqueued on
+    it right after the failed call lands after the batch's writes, every
+    entry.  The next call succeeds with its own results."""
+    import torch
+    from prismdb_amd import crc32c
+    from prismdb_amd._lib import NativeLibraryError
+
+    dev = torch.device("cuda", devices[0])
+    nb = 1 << 18  # 1 GiB of 4 KiB spans: still running when the call returns
+    host = oracle.synth(nb * 4096 + 64, 0x5EED0320)
+    off = np.arange(nb, dtype=np.uint64) * 4096
+    lens = np.full(nb, 4096, dtype=np.uint32)
+    buf, d_off, d_len = _to(dev, host, off, lens)
+    out = torch.zeros(nb, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+    prev = native.prismdb_crc32c_multi_fail_after(0)
+    try:
+        with pytest.raises(NativeLibraryError, match="injected failure"):
+            crc32c.batch_multi([(buf, d_off, d_len)], out=out, check_bounds=False)
+        out.fill_(0x5A5A5A5A)  # on the caller's stream: after the failed call's batch
+    finally:
+        native.prismdb_crc32c_multi_fail_after(prev)
+    torch.cuda.synchronize()
+    assert bool((out == 0x5A5A5A5A).all())
+    want, _ = oracle.batch(host[:64 * 4096], off[:64], lens[:64])
+    out2, _ = crc32c.batch_multi([(buf, d_off, d_len)], check_bounds=False)
+    got = _u32(out2)
+    np.testing.assert_array_equal(got[:64], want)
+    assert len(np.unique(got)) > nb - 64  # every span its own result, not a leftover fill
+
+
+def test_multi_rejects_bad_outputs(devices):
+    """out / mismatch shorter than the partitions' total, of the wrong dtype
+    or not on the root device are rejected before the C ABI writes them."""
+    import torch
+    from prismdb_amd import crc32c
+
+    dev = torch.device("cuda", devices[0])
+    buf = torch.zeros(4096 * 4, dtype=torch.uint8, device=dev)
+    off = torch.arange(4, dtype=torch.int64, device=dev) * 4096
+    lens = torch.full((4,), 4092, dtype=torch.int32, device=dev)
+    for bad in (torch.zeros(3, dtype=torch.int32, device=dev), torch.zeros(4, dtype=torch.int64, device=dev),
+                torch.zeros(4, dtype=torch.int32)):
+        with pytest.raises(ValueError):
+            crc32c.batch_multi([(buf, off, lens)], out=bad)
+    with pytest.raises(ValueError):
+        crc32c.batch_multi([(buf, off, lens)], verify=True, mismatch=torch.zeros(2, dtype=torch.uint8, device=dev))
