@@ -577,7 +577,8 @@ def main() -> int:
               file=sys.stderr)
         return 2
     if os.environ.get("PRISMDB_BENCH_DRYRUN"):  # tests: the launch alone, no GPU
-        print(json.dumps({"dryrun": True, "rank": rank, "world": world, "local_rank": local}), flush=True)
+        # one write(2): lines of concurrent ranks never interleave
+        os.write(1, (json.dumps({"dryrun": True, "rank": rank, "world": world, "local_rank": local}) + "\n").encode())
         return 0
     import torch
     import torch.distributed as dist

@@ -73,6 +73,10 @@ std::atomic<uint64_t> g_direct_max{prismdb::dev::kDirectMaxSpans};
 // whole-span fallback) and its debug flags (DirectWs::dbg).
 std::atomic<uint32_t> g_direct_cap{prismdb::dev::kDirectTickets};
 std::atomic<uint32_t> g_direct_dbg{0};
+// Descriptor batches of more than g_direct_max spans (without LOG_HEADER):
+// windows of the one-launch kernel on two side streams (1) or the planner
+// path (0).
+std::atomic<int> g_windows{1};
 
 void BuildTables(DeviceTables* t) {
   namespace g = prismdb::gf2;
@@ -240,6 +244,12 @@ struct Workspace {
   char* direct = nullptr;  // word, done | ticket map | partials | per-span counters
   uint32_t gen = 0;
   SplitWs ws{};
+  // Bulk descriptor batches: windows of the one-launch kernel alternate
+  // between two side streams (each with its own workspace), forked from and
+  // joined back into this workspace's stream with events.
+  hipStream_t side[2] = {nullptr, nullptr};
+  hipEvent_t fork = nullptr;
+  hipEvent_t join[2] = {nullptr, nullptr};
 };
 
 // A thread that has used more streams than this evicts its least recently
@@ -267,6 +277,14 @@ void SyncAndRelease(Workspace& w) {
   if (hipDeviceGetDefaultMemPool(&pool, w.device) == hipSuccess) (void)hipMemPoolTrimTo(pool, 0);
   for (hipEvent_t ev : w.done)
     if (ev != nullptr) (void)hipEventDestroy(ev);
+  for (int k = 0; k < 2; ++k) {
+    if (w.side[k] != nullptr) {
+      (void)hipStreamSynchronize(w.side[k]);
+      (void)hipStreamDestroy(w.side[k]);
+    }
+    if (w.join[k] != nullptr) (void)hipEventDestroy(w.join[k]);
+  }
+  if (w.fork != nullptr) (void)hipEventDestroy(w.fork);
   if (w.device != cur) (void)hipSetDevice(cur);
   w = Workspace{};
 }
@@ -298,30 +316,20 @@ WorkspaceCache& ThreadWorkspaces() {
   return cache;
 }
 
-Workspace* FindWorkspace(hipStream_t s, int& rc) {
-  WorkspaceCache& cache = ThreadWorkspaces();
-  int device = 0;
-  hipError_t e = hipGetDevice(&device);
-  if (e != hipSuccess) {
-    rc = FailHip(e, "hipGetDevice");
-    return nullptr;
-  }
-  auto& lru = cache.lru;
-  for (auto it = lru.begin(); it != lru.end(); ++it) {
-    if (it->device == device && it->stream == s) {
-      if (it != lru.begin()) lru.splice(lru.begin(), lru, it);
-      rc = 0;
-      return &lru.front();
-    }
-  }
-  if (lru.size() >= kMaxWorkspaces) {
-    SyncAndRelease(lru.back());
-    lru.pop_back();
-  }
-  lru.emplace_front();
-  Workspace& w = lru.front();
+// Streams the engine itself owns and lends to one caller at a time (the host
+// pipeline's ring streams, leased from a per-device pool across threads):
+// their workspace belongs to the stream, not to the calling thread, and is
+// released with it (prismdb::ReleaseEngineStream) -- as thread-local entries
+// they piled up, up to kMaxWorkspaces per thread that ever leased a ring.
+std::mutex g_owned_mu;
+std::list<Workspace> g_owned;  // (list: entries never move)
+std::atomic<int> g_owned_count{0};
+
+// Allocates w's fixed part on stream s (device current).
+int InitWorkspace(Workspace& w, int device, hipStream_t s) {
   w.device = device;
   w.stream = s;
+  hipError_t e = hipSuccess;
   const size_t bytes = 256 + kCapSeg * (16 + 4) + (size_t)kCapLong * (8 + 8 + 4) +
                        (size_t)prismdb::dev::kMaxPlanBlocks * 8;
   e = hipEventCreateWithFlags(&w.done[0], hipEventDisableTiming);
@@ -330,9 +338,8 @@ Workspace* FindWorkspace(hipStream_t s, int& rc) {
   if (e != hipSuccess) {
     for (hipEvent_t ev : w.done)
       if (ev != nullptr) (void)hipEventDestroy(ev);
-    lru.pop_front();
-    rc = FailHip(e, "workspace allocation");
-    return nullptr;
+    w = Workspace{};
+    return FailHip(e, "workspace allocation");
   }
   char* p = static_cast<char*>(w.mem);
   w.ws.counters = reinterpret_cast<SplitCounters*>(p);
@@ -350,8 +357,48 @@ Workspace* FindWorkspace(hipStream_t s, int& rc) {
   w.ws.bsum = reinterpret_cast<uint64_t*>(p);
   w.ws.cap_seg = kCapSeg;
   w.ws.cap_long = kCapLong;
-  rc = 0;
-  return &w;
+  return 0;
+}
+
+
+Workspace* FindWorkspace(hipStream_t s, int& rc) {
+  int device = 0;
+  hipError_t e = hipGetDevice(&device);
+  if (e != hipSuccess) {
+    rc = FailHip(e, "hipGetDevice");
+    return nullptr;
+  }
+  if (g_owned_count.load(std::memory_order_acquire) > 0) {
+    std::lock_guard<std::mutex> lk(g_owned_mu);
+    for (Workspace& w : g_owned) {
+      if (w.stream != s) continue;
+      if (w.mem == nullptr && (rc = InitWorkspace(w, device, s)) != 0) {
+        w.stream = s;  // (stays registered: the next call retries)
+        return nullptr;
+      }
+      rc = 0;
+      return &w;
+    }
+  }
+  WorkspaceCache& cache = ThreadWorkspaces();
+  auto& lru = cache.lru;
+  for (auto it = lru.begin(); it != lru.end(); ++it) {
+    if (it->device == device && it->stream == s) {
+      if (it != lru.begin()) lru.splice(lru.begin(), lru, it);
+      rc = 0;
+      return &lru.front();
+    }
+  }
+  if (lru.size() >= kMaxWorkspaces) {
+    SyncAndRelease(lru.back());
+    lru.pop_back();
+  }
+  lru.emplace_front();
+  if ((rc = InitWorkspace(lru.front(), device, s)) != 0) {
+    lru.pop_front();
+    return nullptr;
+  }
+  return &lru.front();
 }
 
 // Replace *blk (size irrelevant) by a fresh block of `bytes` on stream s; the
@@ -444,6 +491,66 @@ int DirectWorkspace(Workspace& w, hipStream_t s, prismdb::dev::DirectWs* out) {
 
 enum Route { kRouteAuto = 0, kRouteDirect = 1, kRoutePlanner = 2 };
 
+// A descriptor batch of more spans than one launch of the one-launch kernel
+// takes, as ceil(n / wmax) equal windows of consecutive spans, each one
+// launch of that kernel.  Consecutive windows go to two side streams in
+// turn: a window's start-up (table fill, first round trip) then runs while
+// its predecessor drains instead of after it (on one stream the kernel
+// boundary cost ~12 us per window, profiles/r03s_chunked.json).  The side
+// streams start after everything already on s and s waits for both; each
+// side stream has its own workspace, so its windows alternate claim words
+// as any stream's calls do.
+int RunWindows(DeviceCtx& ctx, const SpanBatch& a, bool verify, hipStream_t s, Workspace& w, uint64_t wmax) {
+  hipError_t e = hipSuccess;
+  if (w.fork == nullptr) {
+    for (int k = 0; k < 2 && e == hipSuccess; ++k) {
+      e = hipStreamCreateWithFlags(&w.side[k], hipStreamNonBlocking);
+      if (e == hipSuccess) e = hipEventCreateWithFlags(&w.join[k], hipEventDisableTiming);
+    }
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&w.fork, hipEventDisableTiming);
+    if (e != hipSuccess) {
+      for (int k = 0; k < 2; ++k) {
+        if (w.side[k] != nullptr) (void)hipStreamDestroy(w.side[k]);
+        if (w.join[k] != nullptr) (void)hipEventDestroy(w.join[k]);
+        w.side[k] = nullptr;
+        w.join[k] = nullptr;
+      }
+      w.fork = nullptr;
+      return FailHip(e, "side streams");
+    }
+  }
+  if ((e = hipEventRecord(w.fork, s)) != hipSuccess) return FailHip(e, "fork event");
+  for (int k = 0; k < 2; ++k)
+    if ((e = hipStreamWaitEvent(w.side[k], w.fork, 0)) != hipSuccess) return FailHip(e, "fork wait");
+  const uint64_t cap = 64ull * (uint64_t)ctx.cus * (prismdb::dev::kDirectThreads / 64);  // one span run per wave
+  if (wmax > cap) wmax = cap;
+  const uint64_t nwin = (a.n + wmax - 1) / wmax;
+  int rc = 0;
+  uint64_t at = 0;
+  for (uint64_t k = 0; k < nwin && rc == 0; ++k) {
+    const uint64_t m = (a.n - at) / (nwin - k);  // equal windows, the remainder spread over the last ones
+    SpanBatch p = a;
+    p.off += at;
+    p.len += at;
+    if (p.init != nullptr) p.init += at;
+    if (p.out != nullptr) p.out += at;
+    if (p.mismatch != nullptr) p.mismatch += at;
+    p.n = m;
+    rc = RunBatch(ctx, p, true, verify, w.side[k & 1u], kRouteDirect);
+    at += m;
+  }
+  // joined whatever happened: s never runs ahead of work the call enqueued
+  for (int k = 0; k < 2; ++k) {
+    hipError_t j = hipEventRecord(w.join[k], w.side[k]);
+    if (j == hipSuccess) j = hipStreamWaitEvent(s, w.join[k], 0);
+    if (j != hipSuccess) {
+      (void)hipStreamSynchronize(w.side[k]);
+      if (rc == 0) rc = FailHip(j, "join");
+    }
+  }
+  return rc;
+}
+
 // Launch sequence.  Fixed stride, aligned, <= 4 KiB: one kernel.  Descriptor
 // batches of <= g_direct_max spans: one kernel (crc32c_direct.hip).  The
 // rest: plan (span records, long spans cut into segments) -> span pass (long
@@ -497,6 +604,11 @@ int RunBatch(DeviceCtx& ctx, const SpanBatch& base_args, bool desc, bool verify,
     hipError_t e = prismdb::dev::launch_direct(a, verify, ctx.cus, d, s, w->done[w->gen & 1u]);
     return e == hipSuccess ? 0 : FailHip(e, "direct kernel launch");
   }
+  // Bulk descriptor batches: windows of the one-launch kernel.
+  const uint64_t wmax = g_direct_max.load(std::memory_order_relaxed);
+  if (desc && route == kRouteAuto && wmax > 0 && a.n > wmax && g_windows.load(std::memory_order_relaxed) &&
+      !(a.flags & prismdb::dev::kFlagLogHeader))
+    return RunWindows(ctx, base_args, verify, s, *w, wmax);
   // The span kernel indexes records with 32 bits: cut larger batches.
   if (a.n > prismdb::dev::kMaxGenericSpans) {
     for (uint64_t i = 0; i < a.n; i += prismdb::dev::kMaxGenericSpans) {
@@ -592,6 +704,32 @@ int RunBatch(DeviceCtx& ctx, const SpanBatch& base_args, bool desc, bool verify,
 
 namespace prismdb {
 void SetLastError(const std::string& msg) { t_last_error = msg; }
+
+// The engine's own streams (crc32c_pipeline.hip's rings): one workspace per
+// stream, whichever thread calls on it; released (after its last batch) by
+// ReleaseEngineStream before the stream is destroyed.
+void RegisterEngineStream(hipStream_t s) {
+  std::lock_guard<std::mutex> lk(g_owned_mu);
+  g_owned.emplace_back();
+  g_owned.back().stream = s;
+  g_owned_count.fetch_add(1, std::memory_order_release);
+}
+
+void ReleaseEngineStream(hipStream_t s) {
+  std::list<Workspace> gone;
+  {
+    std::lock_guard<std::mutex> lk(g_owned_mu);
+    for (auto it = g_owned.begin(); it != g_owned.end(); ++it) {
+      if (it->stream == s) {
+        gone.splice(gone.begin(), g_owned, it);
+        g_owned_count.fetch_sub(1, std::memory_order_release);
+        break;
+      }
+    }
+  }
+  for (Workspace& w : gone)
+    if (w.mem != nullptr) SyncAndRelease(w);
+}
 }  // namespace prismdb
 
 extern "C" {
@@ -676,7 +814,8 @@ void prismdb_crc32c_lane_mode(int mode) {
 }
 
 // descriptor batches of at most this many spans take the one-launch kernel
-// (clamped to kDirectMaxSpans; 0: none do); returns the previous value.
+// (clamped to kDirectMaxSpans; 0: none do; larger batches: windows of this
+// many spans, see prismdb_crc32c_windows); returns the previous value.
 uint64_t prismdb_crc32c_direct_max(uint64_t n) {
   if (n > prismdb::dev::kDirectMaxSpans) n = prismdb::dev::kDirectMaxSpans;
   return g_direct_max.exchange(n, std::memory_order_relaxed);
@@ -690,6 +829,11 @@ uint32_t prismdb_crc32c_direct_tickets(uint32_t cap) {
   return g_direct_cap.exchange(cap, std::memory_order_relaxed);
 }
 uint32_t prismdb_crc32c_direct_debug(uint32_t flags) { return g_direct_dbg.exchange(flags, std::memory_order_relaxed); }
+
+// descriptor batches of more than prismdb_crc32c_direct_max spans (log-record
+// batches aside): 1 = windows of the one-launch kernel (default), 0 = the
+// planner path; returns the previous value.
+int prismdb_crc32c_windows(int on) { return g_windows.exchange(on != 0 ? 1 : 0, std::memory_order_relaxed); }
 
 // the call count of the calling thread's workspace for (current device,
 // stream): the next one-launch call there takes gen + 1 (its tag: the low 16

@@ -33,6 +33,10 @@
 
 namespace prismdb {
 void SetLastError(const std::string& msg);  // crc32c_capi.hip: leveldb_crc32c_last_error()
+// crc32c_capi.hip: a ring's compute stream carries its own batch workspace
+// (not one per thread that leases the ring), released with the ring
+void RegisterEngineStream(hipStream_t s);
+void ReleaseEngineStream(hipStream_t s);
 }
 
 namespace {
@@ -73,6 +77,7 @@ struct Slot {
 struct Ring {
   int device = 0;
   hipStream_t copy = nullptr, compute = nullptr;
+  bool registered = false;  // compute's batch workspace (crc32c_capi.hip)
   Slot slot[kDepth];
   // Called with `device` current.  The ring's own streams are drained first;
   // its device blocks go back stream-ordered (no device-wide hipFree).
@@ -89,6 +94,8 @@ struct Ring {
       if (s.done) (void)hipEventDestroy(s.done);
     }
     if (compute) (void)hipStreamSynchronize(compute);
+    // (after the slots: its pool trim then returns their blocks too)
+    if (registered) prismdb::ReleaseEngineStream(compute);
     if (copy) (void)hipStreamDestroy(copy);
     if (compute) (void)hipStreamDestroy(compute);
   }
@@ -97,6 +104,10 @@ struct Ring {
 int MakeRing(Ring& r) {
   hipError_t e = hipStreamCreateWithFlags(&r.copy, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&r.compute, hipStreamNonBlocking);
+  if (e == hipSuccess) {
+    prismdb::RegisterEngineStream(r.compute);
+    r.registered = true;
+  }
   for (Slot& s : r.slot) {
     if (e == hipSuccess) e = hipEventCreateWithFlags(&s.copied, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&s.done, hipEventDisableTiming);

@@ -133,13 +133,17 @@ def native():
 
 
 # Descriptor-batch routes the GPU tests pin (C-ABI test hooks, not public):
-#   direct     the one-launch kernel (crc32c_direct.hip; the default for
-#              batches of <= 2^17 spans)
+#   direct     the one-launch kernel (crc32c_direct.hip; the default: one
+#              launch for batches of <= 2^17 spans, windows of 2^17 spans on
+#              two side streams for larger ones -- log-record batches aside)
+#   windows    the one-launch kernel in windows of 1000 spans (many windows
+#              on modest batches)
 #   lane_log   the planner path, lane kernel in front of log-record batches
-#              (the default for larger batches)
+#              (the default for log-record batches of > 2^17 spans)
 #   lane_all   the planner path, lane kernel in front of every batch
 #   span_only  the planner path alone
-ROUTES = {"direct": (1 << 17, 0), "lane_log": (0, 0), "lane_all": (0, 1), "span_only": (0, -1)}
+ROUTES = {"direct": (1 << 17, 0), "windows": (1000, 0), "lane_log": (0, 0), "lane_all": (0, 1),
+          "span_only": (0, -1)}
 
 
 def set_route(native, name):
@@ -147,17 +151,19 @@ def set_route(native, name):
     direct_max, lane = ROUTES[name]
     native.prismdb_crc32c_direct_max(direct_max)
     native.prismdb_crc32c_lane_mode(lane)
+    native.prismdb_crc32c_windows(1)
 
     def restore():
         native.prismdb_crc32c_direct_max(1 << 17)
         native.prismdb_crc32c_lane_mode(0)
+        native.prismdb_crc32c_windows(1)
 
     return restore
 
 
-@pytest.fixture(params=["direct", "lane_log"])
+@pytest.fixture(params=["direct", "windows", "lane_log"])
 def route(request, native):
-    """The two default descriptor routes: one-launch and planner."""
+    """The default descriptor routes: one-launch (one launch or windows) and planner."""
     restore = set_route(native, request.param)
     yield request.param
     restore()

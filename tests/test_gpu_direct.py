@@ -712,3 +712,61 @@ def test_direct_random_batches(dev, oracle, native, seed):
             expect += (nch + (1 << lg) - 1) >> lg
     d = after - before
     assert d[1] == 0 and d[0] + d[2] + d[3] == expect, (d, expect, n, mode)
+
+
+@pytest.mark.parametrize("mode", ["plain", "seal", "verify"])
+def test_bulk_windows_on_side_streams(dev, oracle, native, mode):
+    """A batch of 300 000 spans (> 2^17: windows of the one-launch kernel on
+    two side streams) on a caller stream that first uploads the bytes: the
+    windows start after the upload, the caller's stream waits for every
+    window (results read there right after the call), and every result,
+    trailer and verify flag equals the oracle's.  Lengths 0-8000 B at any
+    alignment with random init, and 40 spans of 0.2-2 MiB (tickets)."""
+    import torch
+    from prismdb_amd import crc32c
+
+    rng = np.random.default_rng(0x5EED00E0 + len(mode))
+    n = 300_000
+    lens = rng.integers(0, 8000, size=n).astype(np.uint32)
+    lens[rng.choice(n, size=40, replace=False)] = rng.integers(200_000, 2_000_000, size=40)
+    gaps = rng.integers(4, 12, size=n).astype(np.uint64)  # room for a trailer after each span
+    off = (np.cumsum(lens.astype(np.uint64) + gaps) - lens.astype(np.uint64) - gaps + 16).astype(np.uint64)
+    host = oracle.synth(int(off[-1]) + int(lens[-1]) + 64, 0x5EED00E1)
+    init = rng.integers(0, 2**32, size=n, dtype=np.uint64).astype(np.uint32) if mode == "plain" else None
+    raw, _ = oracle.batch(host, off, lens, init)
+    masked = np.array([oracle.mask(int(c)) for c in raw], dtype=np.uint32)
+    tr = (off + lens.astype(np.uint64)).astype(np.int64)[:, None] + np.arange(4)[None, :]
+    if mode == "verify":
+        host[tr] = masked.astype("<u4").view(np.uint8).reshape(-1, 4)
+        bad = rng.choice(n, size=5, replace=False)
+        for i in bad:
+            host[int(off[i])] ^= 0x11  # (an empty span: its stored crc's first byte)
+        raw, _ = oracle.batch(host, off, lens)
+        masked = np.array([oracle.mask(int(c)) for c in raw], dtype=np.uint32)
+    s = torch.cuda.Stream(dev)
+    with torch.cuda.stream(s):
+        buf = torch.empty(len(host), dtype=torch.uint8, device=dev)
+        buf.copy_(torch.from_numpy(host).pin_memory(), non_blocking=True)
+        d_off = torch.from_numpy(off.astype(np.int64)).to(dev)
+        d_len = torch.from_numpy(lens.view(np.int32)).to(dev)
+        d_init = torch.from_numpy(init.view(np.int32)).to(dev) if init is not None else None
+        out = torch.full((n,), 7, dtype=torch.int32, device=dev)
+        mm = torch.full((n,), 7, dtype=torch.uint8, device=dev)
+    if mode == "plain":
+        crc32c.batch(buf, d_off, d_len, d_init, out=out, stream=s, check_bounds=False)
+    elif mode == "seal":
+        crc32c.batch(buf, d_off, d_len, mask=True, trailer=True, out=out, stream=s, check_bounds=False)
+    else:
+        crc32c.batch(buf, d_off, d_len, verify=True, out=out, mismatch=mm, stream=s, check_bounds=False)
+    with torch.cuda.stream(s):
+        got, gmm, gbuf = out.clone(), mm.clone(), buf[:16].clone() if mode != "seal" else buf.clone()
+    s.synchronize()
+    assert _last_split_rc(native) == -2  # one-launch windows
+    np.testing.assert_array_equal(_u32(got), masked if mode == "seal" else raw)
+    if mode == "seal":
+        sealed = gbuf.cpu().numpy()
+        np.testing.assert_array_equal(sealed[tr].copy().view("<u4").reshape(-1), masked)
+    if mode == "verify":
+        want_bad = np.zeros(n, dtype=np.uint8)
+        want_bad[bad] = 1
+        np.testing.assert_array_equal(gmm.cpu().numpy(), want_bad)

@@ -721,6 +721,52 @@ def test_host_pipeline_many_threads(dev, oracle):
     assert not errors, errors
 
 
+def test_host_pipeline_ring_workspaces_released(dev, oracle):
+    """A long-lived thread (this one) calling batch_host next to 7 others,
+    three times: every call leases a ring (8 at once; the pool keeps 2 idle
+    and frees the rest), and the batch workspace of a ring's stream goes
+    with the ring -- it used to stay in each calling thread's cache (up to 8
+    per thread, ~70 MB each), so this thread's device memory grew.  Device
+    memory after the rounds is within 200 MB of before."""
+    import threading
+
+    import torch
+    from prismdb_amd import crc32c
+
+    n = 12000
+    off = np.arange(n, dtype=np.uint64) * 3992
+    lens = np.full(n, 3988, dtype=np.uint32)
+    host = oracle.synth(n * 3992 + 8, 0x5EED0012)
+    raw, _ = oracle.batch(host, off, lens)
+    errors = []
+
+    def run(t):
+        try:
+            got, _ = crc32c.batch_host(host, off, lens)
+            if not (got == raw).all():
+                errors.append(t)
+        except Exception as e:  # noqa: BLE001 - reported below
+            errors.append((t, repr(e)))
+
+    def round_(k):
+        th = [threading.Thread(target=run, args=(t,)) for t in range(k - 1)]
+        for x in th:
+            x.start()
+        run(-1)  # this thread too
+        for x in th:
+            x.join(120)
+
+    round_(2)  # two rings idle in the pool from here on
+    torch.cuda.synchronize()
+    free0, _ = torch.cuda.mem_get_info(dev)
+    for _ in range(3):
+        round_(8)
+    torch.cuda.synchronize()
+    free1, _ = torch.cuda.mem_get_info(dev)
+    assert not errors, errors
+    assert free0 - free1 < 200 << 20, (free0 - free1) / 2**20
+
+
 @pytest.fixture(params=["lane_all", "direct"])
 def short_route(request, native):
     """Short records through the lane kernel (every planner batch) and through

@@ -8,6 +8,7 @@ Prints one JSON object with, per workload, the mean kernel-sequence time
 of the algorithmic bytes (fixed L+4; variable L+4+12; verify
 L+4+1 per span):
   config3_mixed      spans of 1/4/16/64 KiB (uniform, seed 0x5EED0003) packed back to back, ~16 GiB
+  *_planner          the same batch through the planner path (bulk windows of the one-launch kernel off)
   sst_fixed          3988-B spans (YCSB data block + type byte) at stride 3992, 16 Mi spans (~62.4 GiB)
   sst_desc           same spans through descriptors + one 486 977-B index span per 16 811 (split path)
   verify_4k          ReadBlock-verify of 16 Mi x (4092 + type... ) 4 KiB spans with stored trailers
@@ -55,6 +56,16 @@ def main():
         return statistics.median(ts)
 
     res = {}
+    from prismdb_amd._lib import lib as native
+
+    def planner(fn):  # the same call through the planner path (bulk windows off)
+        def run():
+            prev = native().prismdb_crc32c_windows(0)
+            try:
+                fn()
+            finally:
+                native().prismdb_crc32c_windows(prev)
+        return run
 
     def report(name, t, payload, algo, n):
         res[name] = {"spans": n, "payload_GiB": round(payload / GIB, 2), "ms": round(t * 1e3, 3),
@@ -72,8 +83,12 @@ def main():
         off = np.concatenate([[0], np.cumsum(lens)[:-1]])
         d_off, d_len = torch.from_numpy(off).to(dev), torch.from_numpy(lens.astype(np.int32)).to(dev)
         out = torch.empty(len(lens), dtype=torch.int32, device=dev)
-        t = timed(lambda: crc32c.batch(buf, d_off, d_len, out=out, check_bounds=False), args.reps)
-        report("config3_mixed", t, lens.sum(), lens.sum() + 16 * len(lens), len(lens))
+        fn = lambda: crc32c.batch(buf, d_off, d_len, out=out, check_bounds=False)  # noqa: E731
+        report("config3_mixed", timed(fn, args.reps), lens.sum(), lens.sum() + 16 * len(lens), len(lens))
+        ref = out.clone()
+        report("config3_mixed_planner", timed(planner(fn), args.reps), lens.sum(), lens.sum() + 16 * len(lens),
+               len(lens))
+        res["config3_mixed_planner"]["agrees"] = bool(torch.equal(ref, out))
         del d_off, d_len, out
 
     # SST-shaped, fixed stride
@@ -102,8 +117,11 @@ def main():
         assert off[-1] + lens[-1] + 4 <= buf.numel()
         d_off, d_len = torch.from_numpy(off).to(dev), torch.from_numpy(lens.astype(np.int32)).to(dev)
         out2 = torch.empty(len(off), dtype=torch.int32, device=dev)
-        t = timed(lambda: crc32c.batch(buf, d_off, d_len, out=out2, mask=True, check_bounds=False), args.reps)
-        report("sst_desc", t, lens.sum(), lens.sum() + 16 * len(lens), len(lens))
+        fn = lambda: crc32c.batch(buf, d_off, d_len, out=out2, mask=True, check_bounds=False)  # noqa: E731
+        report("sst_desc", timed(fn, args.reps), lens.sum(), lens.sum() + 16 * len(lens), len(lens))
+        ref = out2.clone()
+        report("sst_desc_planner", timed(planner(fn), args.reps), lens.sum(), lens.sum() + 16 * len(lens), len(lens))
+        res["sst_desc_planner"]["agrees"] = bool(torch.equal(ref, out2))
         del d_off, d_len, out2
 
     # verify 4 KiB spans (fixed stride 4096, span 4092 B, trailer in the last 4 B)
@@ -120,8 +138,11 @@ def main():
     if want("adversarial"):
         d_off, d_len = torch.from_numpy(off).to(dev), torch.from_numpy(lens.astype(np.int32)).to(dev)
         out3 = torch.empty(m, dtype=torch.int32, device=dev)
-        t = timed(lambda: crc32c.batch(buf, d_off, d_len, out=out3, check_bounds=False), args.reps)
-        report("adversarial", t, lens.sum(), lens.sum() + 16 * m, m)
+        fn = lambda: crc32c.batch(buf, d_off, d_len, out=out3, check_bounds=False)  # noqa: E731
+        report("adversarial", timed(fn, args.reps), lens.sum(), lens.sum() + 16 * m, m)
+        ref = out3.clone()
+        report("adversarial_planner", timed(planner(fn), args.reps), lens.sum(), lens.sum() + 16 * m, m)
+        res["adversarial_planner"]["agrees"] = bool(torch.equal(ref, out3))
 
         del d_off, d_len, out3
 

@@ -10,7 +10,7 @@ descriptors in, tables in, slot 0's data in, first fold done, ring drained,
 exit): percentiles
 over the waves with a static run, and the latest exit of any wave.
 
-    python tools/direct_timeline.py [--lib tools/_build/variants/lib_direct_ts.so] [--data-only]
+    python tools/direct_timeline.py [--lib tools/vlib/lib_direct_ts.so] [--data-only]
 """
 import argparse
 import ctypes

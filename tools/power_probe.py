@@ -19,7 +19,7 @@ import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-VDIR = os.path.join(ROOT, "tools", "_build", "variants")
+VDIR = os.path.join(ROOT, "tools", "vlib")
 
 
 def sampler(stop, path):

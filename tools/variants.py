@@ -1,11 +1,13 @@
 #!/usr/bin/env python3
 """Compare variants of the engine in ONE process, interleaved.
 
-    python tools/variants.py build [--only a b]     # here: build tools/_build/variants/lib_*.so
+    python tools/variants.py build [--only a b]     # here: build tools/vlib/lib_*.so
     python tools/variants.py run [--gib 64] ...     # GPU box: time them on one buffer
 
 A variant is the full library built from a PATCHED COPY of the sources
-(tools/_build/variants/<name>/pkg/csrc): each entry of VARIANTS lists exact
+(build/variants/<name>/pkg/csrc; the libraries go to tools/vlib/, which
+ships to the GPU box: `build` empties it first, so only the variants built
+last travel): each entry of VARIANTS lists exact
 text substitutions (file, old, new), each of which must match exactly once.
 Measurement-only variants (marked "wrong results") exist only here, never as
 knobs in the product source.  Each library is loaded with RTLD_LOCAL and
@@ -27,7 +29,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-VDIR = os.path.join(ROOT, "tools", "_build", "variants")
+VDIR = os.path.join(ROOT, "tools", "vlib")
 
 # Measurement-only variants compute wrong results on purpose: their device
 # self-test would refuse the device, so it is reported but not enforced.
@@ -151,6 +153,14 @@ VARIANTS = {
          "                 lane == 5 ? ts5 : lane == 6 ? (uint64_t)m : tsw;\n"
          "    reinterpret_cast<uint64_t*>(a.out + ((n + 3u) & ~3u))[8u * wave + lane] = v;\n  }\n}\n\nhipError_t launch_direct"),
     ] + MEASURE_ONLY,
+    # the one-launch kernel's slot 1 issued only once slot 0 has landed: the
+    # memory system then serves every wave's first three tasks first (37 MB)
+    # instead of interleaving all 67 MB of a file, and slot 0's folds overlap
+    # slot 1's loads instead of all folds bunching at the end
+    "slot1_late": [("crc32c_direct.hip",
+                    "        // slot 0 went out before the table fill; slot 1 now\n",
+                    "        // slot 0 went out before the table fill; slot 1 once it has landed\n"
+                    "#pragma unroll\n        for (int st = 0; st < 3; ++st) wait_task<0>(wb[0][st], eb[0][st]);\n")],
 }
 
 # the previous commit's kernels (a git worktree under build/:
@@ -159,10 +169,16 @@ VARIANTS["prev"] = [("@src", os.path.join(ROOT, "build", "wt_head", "prismdb_amd
 # combinations
 VARIANTS["tf_ts"] = VARIANTS["tables_first"] + VARIANTS["direct_ts"]
 VARIANTS["tf_lg0_w2"] = VARIANTS["tables_first"] + VARIANTS["lg0"] + VARIANTS["workers2x"]
+VARIANTS["tf_s1l"] = VARIANTS["tables_first"] + VARIANTS["slot1_late"]
 
 
 def do_build(names):
     from prismdb_amd.build import CSRC, build
+
+    os.makedirs(VDIR, exist_ok=True)
+    for f in os.listdir(VDIR):  # only this build's variants ship with the next GPU call
+        if f.startswith("lib_") and f.endswith(".so"):
+            os.remove(os.path.join(VDIR, f))
 
     for name in names:
         if name not in VARIANTS:
