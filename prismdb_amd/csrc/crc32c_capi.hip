@@ -23,6 +23,13 @@
 #include "crc32c_device.h"
 #include "crc32c_gf2.h"
 
+namespace prismdb {
+// Streams the engine creates for itself (pipeline rings, bulk-window side
+// streams, batch_multi cliques) carry their own workspace: defined below.
+void RegisterEngineStream(hipStream_t s);
+void ReleaseEngineStream(hipStream_t s);
+}  // namespace prismdb
+
 namespace {
 
 using prismdb::dev::DeviceTables;
@@ -280,6 +287,7 @@ void SyncAndRelease(Workspace& w) {
   for (int k = 0; k < 2; ++k) {
     if (w.side[k] != nullptr) {
       (void)hipStreamSynchronize(w.side[k]);
+      prismdb::ReleaseEngineStream(w.side[k]);
       (void)hipStreamDestroy(w.side[k]);
     }
     if (w.join[k] != nullptr) (void)hipEventDestroy(w.join[k]);
@@ -317,10 +325,12 @@ WorkspaceCache& ThreadWorkspaces() {
 }
 
 // Streams the engine itself owns and lends to one caller at a time (the host
-// pipeline's ring streams, leased from a per-device pool across threads):
+// pipeline's ring streams, leased from a per-device pool across threads; the
+// side streams of a workspace's bulk windows; batch_multi's clique streams):
 // their workspace belongs to the stream, not to the calling thread, and is
 // released with it (prismdb::ReleaseEngineStream) -- as thread-local entries
-// they piled up, up to kMaxWorkspaces per thread that ever leased a ring.
+// they piled up (up to kMaxWorkspaces per thread that ever leased a ring) or
+// cycled through the LRU.
 std::mutex g_owned_mu;
 std::list<Workspace> g_owned;  // (list: entries never move)
 std::atomic<int> g_owned_count{0};
@@ -507,7 +517,12 @@ int RunWindows(DeviceCtx& ctx, const SpanBatch& a, bool verify, hipStream_t s, W
       e = hipStreamCreateWithFlags(&w.side[k], hipStreamNonBlocking);
       if (e == hipSuccess) e = hipEventCreateWithFlags(&w.join[k], hipEventDisableTiming);
     }
+    // (a side stream's workspace is the stream's, outside the thread's LRU:
+    // batch_multi's N devices x (clique stream + 2 side streams) would
+    // otherwise cycle through kMaxWorkspaces entries on every call)
     if (e == hipSuccess) e = hipEventCreateWithFlags(&w.fork, hipEventDisableTiming);
+    if (e == hipSuccess)
+      for (int k = 0; k < 2; ++k) prismdb::RegisterEngineStream(w.side[k]);
     if (e != hipSuccess) {
       for (int k = 0; k < 2; ++k) {
         if (w.side[k] != nullptr) (void)hipStreamDestroy(w.side[k]);
@@ -705,9 +720,11 @@ int RunBatch(DeviceCtx& ctx, const SpanBatch& base_args, bool desc, bool verify,
 namespace prismdb {
 void SetLastError(const std::string& msg) { t_last_error = msg; }
 
-// The engine's own streams (crc32c_pipeline.hip's rings): one workspace per
-// stream, whichever thread calls on it; released (after its last batch) by
-// ReleaseEngineStream before the stream is destroyed.
+// The engine's own streams (pipeline rings, window side streams, clique
+// streams): one workspace per stream, whichever thread calls on it (one at
+// a time: a leased ring, the owning workspace's thread, the clique's mutex);
+// released (after its last batch) by ReleaseEngineStream before the stream
+// is destroyed.
 void RegisterEngineStream(hipStream_t s) {
   std::lock_guard<std::mutex> lk(g_owned_mu);
   g_owned.emplace_back();

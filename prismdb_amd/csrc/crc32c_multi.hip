@@ -29,6 +29,7 @@
 
 namespace prismdb {
 void SetLastError(const std::string& msg);  // crc32c_capi.hip: leveldb_crc32c_last_error()
+void RegisterEngineStream(hipStream_t s);   // crc32c_capi.hip: the stream's own batch workspace
 }
 
 namespace {
@@ -86,6 +87,7 @@ int GetClique(int ndev, const int* devices, Clique** out) {
   for (int p = 0; p < ndev; ++p) {
     hipError_t e = hipSetDevice(devices[p]);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->streams[p], hipStreamNonBlocking);
+    if (e == hipSuccess) prismdb::RegisterEngineStream(c->streams[p]);  // (used under the clique's mutex)
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->events[p], hipEventDisableTiming);
     if (e != hipSuccess) {
       (void)hipSetDevice(cur);

@@ -24,7 +24,7 @@ sys.path.insert(0, ROOT)
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--lib", default=os.path.join(ROOT, "tools", "_build", "variants", "lib_direct_ts.so"))
+    ap.add_argument("--lib", default=os.path.join(ROOT, "tools", "vlib", "lib_direct_ts.so"))
     ap.add_argument("--data-only", action="store_true", help="no index span")
     args = ap.parse_args()
     import numpy as np

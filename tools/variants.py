@@ -161,6 +161,10 @@ VARIANTS = {
                     "        // slot 0 went out before the table fill; slot 1 now\n",
                     "        // slot 0 went out before the table fill; slot 1 once it has landed\n"
                     "#pragma unroll\n        for (int st = 0; st < 3; ++st) wait_task<0>(wb[0][st], eb[0][st]);\n")],
+    # the one-launch kernel with a ring of four single-task slots (one task
+    # sequence, waits for the oldest task only) instead of two slots of three
+    # streams (tools/patches/crc32c_direct_ring4.hip)
+    "ring4": [("crc32c_direct.hip", "@file", "tools/patches/crc32c_direct_ring4.hip")],
 }
 
 # the previous commit's kernels (a git worktree under build/:
@@ -170,6 +174,18 @@ VARIANTS["prev"] = [("@src", os.path.join(ROOT, "build", "wt_head", "prismdb_amd
 VARIANTS["tf_ts"] = VARIANTS["tables_first"] + VARIANTS["direct_ts"]
 VARIANTS["tf_lg0_w2"] = VARIANTS["tables_first"] + VARIANTS["lg0"] + VARIANTS["workers2x"]
 VARIANTS["tf_s1l"] = VARIANTS["tables_first"] + VARIANTS["slot1_late"]
+VARIANTS["tf_s1l_ts"] = VARIANTS["tf_s1l"] + VARIANTS["direct_ts"]
+VARIANTS["ring4_ts"] = VARIANTS["ring4"] + [
+    e if "tk[sl][0].valid()" not in e[1] and "wait_task<0>(wb[sl][st]" not in e[1] else
+    (e[0],
+     "            if (tk[q].valid()) fold(tk[q], wb[q], eb[q]);\n" if "tk[sl][0]" in e[1] else
+     "        for (int q = 0; q < 4; ++q) wait_task<0>(wb[q], eb[q]);\n      }\n",
+     ("            if (tsw == 0) tsw = __builtin_amdgcn_s_memrealtime();\n"
+      "            if (tk[q].valid()) fold(tk[q], wb[q], eb[q]);\n"
+      "            if (ts3 == 0) ts3 = __builtin_amdgcn_s_memrealtime();\n") if "tk[sl][0]" in e[1] else
+     ("        for (int q = 0; q < 4; ++q) wait_task<0>(wb[q], eb[q]);\n      }\n"
+      "        ts4 = __builtin_amdgcn_s_memrealtime();\n"))
+    for e in VARIANTS["direct_ts"]]
 
 
 def do_build(names):
@@ -197,6 +213,9 @@ def do_build(names):
             os.symlink(os.path.join(ROOT, "include"), inc)
         for fname, old, new in spec:
             path = os.path.join(src, fname)
+            if old == "@file":  # (fname, "@file", path): the whole file replaced by a copy under tools/patches
+                shutil.copyfile(os.path.join(ROOT, new), path)
+                continue
             with open(path) as f:
                 text = f.read()
             if text.count(old) != 1:
