@@ -197,8 +197,8 @@ def cpu_baseline_leg(args, gpu_out, dev_buf) -> dict | None:
         big = dev_buf[:nall * BLOCK].cpu().numpy()
         oall = np.empty(nall, dtype=np.uint32)
         nthr = len(cpus)
-        t_one = max(t1 * nall / nblk / nthr, 1e-6)  # ~wall seconds of one pass on nthr threads
-        p_all = max(1, int(round(2.0 / t_one)))  # ~2 s of wall time
+        t_one = max(run(nthr, 1, big, oall, nall), 1e-6)  # one calibration pass: the box may give this
+        p_all = max(1, min(64, int(round(2.0 / t_one))))  # process fewer cores than its affinity set; ~2 s
         ta = run(nthr, p_all, big, oall, nall)
         ga = gpu_out[:nall].cpu().numpy().view(np.uint32)
         res["all_cores"] = {

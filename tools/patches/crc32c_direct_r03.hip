@@ -362,7 +362,7 @@ __global__ __launch_bounds__(kDirectThreads) void crc32c_direct_kernel(SpanBatch
         t.f += 1u << 22;
         return t;
       }
-      const uint64_t par = st >= 3u ? ~0ull : 0x9249249249249249ull << st;  // positions st mod 3 (3: all)
+      const uint64_t par = 0x9249249249249249ull << st;  // positions st mod 3
       const uint64_t from = j >= 64u ? 0ull : ~0ull << j;
       const uint64_t avail = shortm & par & from;
       if (avail == 0u) {
@@ -379,7 +379,7 @@ __global__ __launch_bounds__(kDirectThreads) void crc32c_direct_kernel(SpanBatch
       t.b = sbase + p;
       t.c = 0;  // (the ring reads the chunk from f)
       t.c1 = 1;
-      j = p + (st >= 3u ? 1u : 3u);
+      j = p + 3u;
       return t;
     };
     // 17 loads per task, always: 16 body dwords of chunk t.c (the buffer
@@ -424,29 +424,23 @@ __global__ __launch_bounds__(kDirectThreads) void crc32c_direct_kernel(SpanBatch
       if (kVerify && last && lane >= 6u && lane < 10u) eoff = hwin ? lane - 6u : sat((uint64_t)len + (lane - 6u));
       e = buf_ubyte(re, eoff);
     };
-    // One sequence of tasks (run positions in order, a span's chunks one
-    // after another) through a ring of four single-task slots: a wave waits
-    // for its OLDEST task only (three younger tasks, 51 loads, stay in
-    // flight) and folds it as soon as it has landed, instead of waiting for
-    // three tasks at once -- the folds then follow the data as it arrives.
-    DTask tk[4];
-    uint32_t wb[4][kRounds];
-    uint32_t eb[4];
-    uint32_t jc = 0u;
-    {
+    DTask tk[2][3];
+    uint32_t wb[2][3][kRounds];
+    uint32_t eb[2][3];
+    uint32_t jc[3] = {0u, 1u, 2u};
+#pragma unroll
+    for (int st = 0; st < 3; ++st) {
       DTask none = geometry(base, 0u);
       none.f = 0;
-      tk[0] = static_task(jc, 3u, none);  // (none without a run)
-      tk[1] = static_task(jc, 3u, tk[0]);
-      tk[2] = static_task(jc, 3u, tk[1]);
-      tk[3] = static_task(jc, 3u, tk[2]);
+      tk[0][st] = static_task(jc[st], (uint32_t)st, none);  // (none without a run)
+      tk[1][st] = static_task(jc[st], (uint32_t)st, tk[0][st]);
     }
     // Every wave runs the ring (a wave without a run: empty tasks, whose
     // range-checked loads touch no memory, and no folds), so the ring's
     // registers have one definition on every path: hipCC then never copies
     // an in-flight register at a merge (tools/check_inflight.py).
 #pragma unroll
-    for (int q = 0; q < 3; ++q) issue(tk[q], wb[q], eb[q]);
+    for (int st = 0; st < 3; ++st) issue(tk[0][st], wb[0][st], eb[0][st]);
     tables_wait<3 * (kRounds + 1)>(tr);  // slot 0's 51 loads stay in flight
     tables_store<kDirectThreads>(lds, tr, tid);
     // Group barrier for the LDS image.  Not __syncthreads(): its release
@@ -679,44 +673,65 @@ __global__ __launch_bounds__(kDirectThreads) void crc32c_direct_kernel(SpanBatch
     // With 12 waves per CU, an SST file's ~5.6 spans per wave are all
     // requested at once.
     {
-      // the register between the chunks of the current span
-      uint32_t carry = 0u;
-      auto fold = [&](const DTask& t, uint32_t (&w)[kRounds], const uint32_t e) {
-        // the initial register, fed the head bytes, enters chunk 0 with its
-        // body word 0 (a zero injection for a later chunk, which continues
-        // the carried register); realigned and reduced every task, and a
-        // span's last chunk finishes it
-        const bool c0 = t.rc() == 0u;
-        const uint32_t r =
-            feed_short(ss, lane, readlane(vinit, t.slot()) ^ kConditioning, edge_head(e, t.h()), t.h());
-        uint32_t acc = c0 ? 0u : carry;
-        if (t.z) inject(w, t.pad(), c0 ? r : 0u);
+      // a stream's register between the chunks of its current span
+      uint32_t carry[3] = {0u, 0u, 0u};
+      auto fold = [&](const DTask (&t)[3], uint32_t (&w)[3][kRounds], const uint32_t (&e)[3]) {
+        // Per stream, unconditionally (three independent chains; under
+        // per-stream branches the head feeds and the realignments ran one
+        // after the other): the initial register, fed the head bytes, enters
+        // chunk 0 with its body word 0 (a zero injection for a later chunk,
+        // which continues its stream's carried register); every stream is
+        // realigned and reduced, and a span's last chunk finishes it.
+        uint32_t r[3], acc[3];
 #pragma unroll
-        for (int j = 0; j < kRounds; ++j) acc = step256(lds, tab, acc, w[j]);
-        const uint32_t v = realign(lds, nibtab, acc);
-        carry = acc;
-        const uint32_t bv = wave_xor(v);
-        if (t.valid() && t.rlast()) finish(t, t.z ? bv : r, edge_tail(e, t.t()), edge_stored(e), true);
+        for (int st = 0; st < 3; ++st) {
+          const bool c0 = t[st].rc() == 0u;
+          r[st] = feed_short(ss, lane, readlane(vinit, t[st].slot()) ^ kConditioning, edge_head(e[st], t[st].h()),
+                             t[st].h());
+          acc[st] = c0 ? 0u : carry[st];
+          if (t[st].z) inject(w[st], t[st].pad(), c0 ? r[st] : 0u);
+        }
+#pragma unroll
+        for (int j = 0; j < kRounds; ++j) {
+#pragma unroll
+          for (int st = 0; st < 3; ++st) acc[st] = step256(lds, tab, acc[st], w[st][j]);
+        }
+        uint32_t v[3];
+#pragma unroll
+        for (int st = 0; st < 3; ++st) v[st] = realign(lds, nibtab, acc[st]);
+#pragma unroll
+        for (int st = 0; st < 3; ++st) {
+          carry[st] = acc[st];
+          const uint32_t bv = wave_xor(v[st]);
+          if (t[st].valid() && t[st].rlast())
+            finish(t[st], t[st].z ? bv : r[st], edge_tail(e[st], t[st].t()), edge_stored(e[st]), true);
+        }
       };
       {
-        // three tasks went out before the table fill; the fourth now
-        issue(tk[3], wb[3], eb[3]);
-        constexpr int kYounger = 3 * (kRounds + 1);  // the three younger tasks
+        // slot 0 went out before the table fill; slot 1 now
+#pragma unroll
+        for (int st = 0; st < 3; ++st) issue(tk[1][st], wb[1][st], eb[1][st]);
+        constexpr int kYounger = 3 * (kRounds + 1);  // the other slot's three tasks
         static_assert(kYounger <= 63, "vmcnt counts at most 63 loads");
         for (;;) {
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            wait_task<kYounger>(wb[q], eb[q]);
-            if (tk[q].valid()) fold(tk[q], wb[q], eb[q]);
-            // tasks are made in sequence: the next one invalid, all are
-            if (!tk[(q + 1) & 3].valid()) goto drained;
-            tk[q] = static_task(jc, 3u, tk[(q + 3) & 3]);
-            issue(tk[q], wb[q], eb[q]);
+          for (int sl = 0; sl < 2; ++sl) {
+#pragma unroll
+            for (int st = 0; st < 3; ++st) wait_task<kYounger>(wb[sl][st], eb[sl][st]);
+            if (tk[sl][0].valid() || tk[sl][1].valid() || tk[sl][2].valid()) fold(tk[sl], wb[sl], eb[sl]);
+            if (!tk[sl ^ 1][0].valid() && !tk[sl ^ 1][1].valid() && !tk[sl ^ 1][2].valid()) goto drained;
+#pragma unroll
+            for (int st = 0; st < 3; ++st) tk[sl][st] = static_task(jc[st], (uint32_t)st, tk[sl ^ 1][st]);
+#pragma unroll
+            for (int st = 0; st < 3; ++st) issue(tk[sl][st], wb[sl][st], eb[sl][st]);
           }
         }
       drained:
 #pragma unroll
-        for (int q = 0; q < 4; ++q) wait_task<0>(wb[q], eb[q]);
+        for (int sl = 0; sl < 2; ++sl) {
+#pragma unroll
+          for (int st = 0; st < 3; ++st) wait_task<0>(wb[sl][st], eb[sl][st]);
+        }
       }
     }
 

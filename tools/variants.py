@@ -138,13 +138,13 @@ VARIANTS = {
          "    asm volatile(\"s_waitcnt lgkmcnt(0)\\n\\ts_barrier\" ::: \"memory\");\n"
          "    ts2 = __builtin_amdgcn_s_memrealtime();\n"),
         ("crc32c_direct.hip",
-         "            if (tk[sl][0].valid() || tk[sl][1].valid() || tk[sl][2].valid()) fold(tk[sl], wb[sl], eb[sl]);\n",
+         "            if (tk[q].valid()) fold(tk[q], wb[q], eb[q]);\n",
          "            if (tsw == 0) tsw = __builtin_amdgcn_s_memrealtime();\n"
-         "            if (tk[sl][0].valid() || tk[sl][1].valid() || tk[sl][2].valid()) fold(tk[sl], wb[sl], eb[sl]);\n"
+         "            if (tk[q].valid()) fold(tk[q], wb[q], eb[q]);\n"
          "            if (ts3 == 0) ts3 = __builtin_amdgcn_s_memrealtime();\n"),
         ("crc32c_direct.hip",
-         "          for (int st = 0; st < 3; ++st) wait_task<0>(wb[sl][st], eb[sl][st]);\n        }\n",
-         "          for (int st = 0; st < 3; ++st) wait_task<0>(wb[sl][st], eb[sl][st]);\n        }\n"
+         "        for (int q = 0; q < 4; ++q) wait_task<0>(wb[q], eb[q]);\n      }\n",
+         "        for (int q = 0; q < 4; ++q) wait_task<0>(wb[q], eb[q]);\n      }\n"
          "        ts4 = __builtin_amdgcn_s_memrealtime();\n"),
         ("crc32c_direct.hip", "    }\n  }\n\n}\n\nhipError_t launch_direct",
          "    }\n  }\n  if (a.out != nullptr && lane < 8u) {\n"
@@ -161,10 +161,25 @@ VARIANTS = {
                     "        // slot 0 went out before the table fill; slot 1 now\n",
                     "        // slot 0 went out before the table fill; slot 1 once it has landed\n"
                     "#pragma unroll\n        for (int st = 0; st < 3; ++st) wait_task<0>(wb[0][st], eb[0][st]);\n")],
-    # the one-launch kernel with a ring of four single-task slots (one task
-    # sequence, waits for the oldest task only) instead of two slots of three
-    # streams (tools/patches/crc32c_direct_ring4.hip)
-    "ring4": [("crc32c_direct.hip", "@file", "tools/patches/crc32c_direct_ring4.hip")],
+    # the one-launch kernel before round 4's ring change: two slots of three
+    # streams (tools/patches/crc32c_direct_r03.hip, the round-3 source)
+    "ring6": [("crc32c_direct.hip", "@file", "tools/patches/crc32c_direct_r03.hip")],
+    # one task (17 loads) in flight before the table barrier instead of three:
+    # the barrier then waits on fewer queued loads, the other three tasks go
+    # out right after it
+    "t1": [("crc32c_direct.hip",
+            "#pragma unroll\n    for (int q = 0; q < 3; ++q) issue(tk[q], wb[q], eb[q]);\n"
+            "    tables_wait<3 * (kRounds + 1)>(tr);  // the three tasks' 51 loads stay in flight\n",
+            "    issue(tk[0], wb[0], eb[0]);\n    tables_wait<kRounds + 1>(tr);\n"),
+           ("crc32c_direct.hip", "        issue(tk[3], wb[3], eb[3]);\n",
+            "#pragma unroll\n        for (int q = 1; q < 4; ++q) issue(tk[q], wb[q], eb[q]);\n")],
+    # the table fill retired before any data load
+    "t0": [("crc32c_direct.hip",
+            "#pragma unroll\n    for (int q = 0; q < 3; ++q) issue(tk[q], wb[q], eb[q]);\n"
+            "    tables_wait<3 * (kRounds + 1)>(tr);  // the three tasks' 51 loads stay in flight\n",
+            "    tables_wait<0>(tr);\n"),
+           ("crc32c_direct.hip", "        issue(tk[3], wb[3], eb[3]);\n",
+            "#pragma unroll\n        for (int q = 0; q < 4; ++q) issue(tk[q], wb[q], eb[q]);\n")],
 }
 
 # the previous commit's kernels (a git worktree under build/:
@@ -173,19 +188,8 @@ VARIANTS["prev"] = [("@src", os.path.join(ROOT, "build", "wt_head", "prismdb_amd
 # combinations
 VARIANTS["tf_ts"] = VARIANTS["tables_first"] + VARIANTS["direct_ts"]
 VARIANTS["tf_lg0_w2"] = VARIANTS["tables_first"] + VARIANTS["lg0"] + VARIANTS["workers2x"]
-VARIANTS["tf_s1l"] = VARIANTS["tables_first"] + VARIANTS["slot1_late"]
-VARIANTS["tf_s1l_ts"] = VARIANTS["tf_s1l"] + VARIANTS["direct_ts"]
-VARIANTS["ring4_ts"] = VARIANTS["ring4"] + [
-    e if "tk[sl][0].valid()" not in e[1] and "wait_task<0>(wb[sl][st]" not in e[1] else
-    (e[0],
-     "            if (tk[q].valid()) fold(tk[q], wb[q], eb[q]);\n" if "tk[sl][0]" in e[1] else
-     "        for (int q = 0; q < 4; ++q) wait_task<0>(wb[q], eb[q]);\n      }\n",
-     ("            if (tsw == 0) tsw = __builtin_amdgcn_s_memrealtime();\n"
-      "            if (tk[q].valid()) fold(tk[q], wb[q], eb[q]);\n"
-      "            if (ts3 == 0) ts3 = __builtin_amdgcn_s_memrealtime();\n") if "tk[sl][0]" in e[1] else
-     ("        for (int q = 0; q < 4; ++q) wait_task<0>(wb[q], eb[q]);\n      }\n"
-      "        ts4 = __builtin_amdgcn_s_memrealtime();\n"))
-    for e in VARIANTS["direct_ts"]]
+VARIANTS["t1_ts"] = VARIANTS["t1"] + VARIANTS["direct_ts"]
+VARIANTS["t0_ts"] = VARIANTS["t0"] + VARIANTS["direct_ts"]
 
 
 def do_build(names):
