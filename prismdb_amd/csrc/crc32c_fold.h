@@ -85,13 +85,12 @@ __device__ __forceinline__ uint32_t feed_short(const ShortShift& ss, uint32_t la
 }
 
 // The caller owns the span's trailer bytes when it asks for them to be written
-// (TableBuilder::WriteRawBlock, table/table_builder.cc:196).
+// (TableBuilder::WriteRawBlock, table/table_builder.cc:196): one dword store
+// at any byte alignment (the hardware splits a misaligned one; as four byte
+// stores each trailer was four write requests -- the lane kernel's log-header
+// stores were always one).  Little-endian, so the bytes are EncodeFixed32's.
 __device__ __forceinline__ void store_le32(const uint8_t* p, uint32_t v) {
-  uint8_t* q = const_cast<uint8_t*>(p);
-  q[0] = (uint8_t)v;
-  q[1] = (uint8_t)(v >> 8);
-  q[2] = (uint8_t)(v >> 16);
-  q[3] = (uint8_t)(v >> 24);
+  asm volatile("global_store_dword %0, %1, off" : : "v"(p), "v"(v) : "memory");
 }
 
 __device__ __forceinline__ uint32_t mask_crc(uint32_t c) { return ((c << 17) | (c >> 15)) + kMaskDelta; }

@@ -175,3 +175,21 @@ def any_route(request, native):
     restore = set_route(native, request.param)
     yield request.param
     restore()
+
+
+@pytest.fixture(params=["windows", "planner"])
+def bulk_route(request, native):
+    """Batches of more than 2^17 spans: windows of the one-launch kernel (the
+    default) and the planner path (windows off)."""
+    prev = native.prismdb_crc32c_windows(1 if request.param == "windows" else 0)
+    yield request.param
+    native.prismdb_crc32c_windows(prev)
+
+
+@pytest.fixture
+def planner_bulk(native):
+    """Pin the planner path for batches of more than 2^17 spans (tests of its
+    own machinery: pair runs, slices, the segment workspace)."""
+    prev = native.prismdb_crc32c_windows(0)
+    yield "planner"
+    native.prismdb_crc32c_windows(prev)

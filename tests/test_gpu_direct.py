@@ -434,21 +434,26 @@ def test_late_push_and_orphans(dev, oracle, native, dbg):
 
 
 def test_direct_limit(dev, oracle, native):
-    """2^17 spans (the one-launch limit) take the one-launch path, 2^17 + 1 the
-    planner; both bit-exact on the same mix of short and long spans."""
+    """2^17 spans (the one-launch limit) take one launch, 2^17 + 1 two
+    windows of the same kernel, and with the windows off the planner; all
+    bit-exact on the same mix of short and long spans."""
     import torch
     from prismdb_amd import crc32c
 
     rng = np.random.default_rng(0x5EED00D8)
     size = 64 << 20
     host = oracle.synth(size, 0x5EED00D8)
-    for n, rc in ((1 << 17, -2), ((1 << 17) + 1, 0)):
+    for n, windows, rc in ((1 << 17, 1, -2), ((1 << 17) + 1, 1, -2), ((1 << 17) + 1, 0, 0)):
         lens = rng.integers(0, 4500, size=n).astype(np.uint64)
         lens[rng.integers(0, n, size=20)] = rng.integers(4500, 200_000, size=20)
         off = rng.integers(0, size - 200_001, size=n).astype(np.uint64)
         want, _ = oracle.batch(host, off, lens)
-        out, _ = crc32c.batch(torch.from_numpy(host).to(dev), torch.from_numpy(off.astype(np.int64)).to(dev),
-                              torch.from_numpy(lens.astype(np.uint32).view(np.int32)).to(dev))
+        prev = native.prismdb_crc32c_windows(windows)
+        try:
+            out, _ = crc32c.batch(torch.from_numpy(host).to(dev), torch.from_numpy(off.astype(np.int64)).to(dev),
+                                  torch.from_numpy(lens.astype(np.uint32).view(np.int32)).to(dev))
+        finally:
+            native.prismdb_crc32c_windows(prev)
         assert _last_split_rc(native) == rc
         np.testing.assert_array_equal(_u32(out), want)
 

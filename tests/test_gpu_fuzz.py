@@ -151,7 +151,7 @@ def test_random_fixed_geometry(dev, oracle, native, seed):
 
 
 @pytest.mark.parametrize("seed", SEEDS[:max(4, len(SEEDS) // 3)])
-def test_random_pair_batches(dev, oracle, native, seed):
+def test_random_pair_batches(dev, oracle, native, seed, planner_bulk):
     """Random batches the pair-run span kernel takes: >= 2^18 spans, each one
     task (0..4096 B at any alignment) or long (split path, 1 in 2000), at
     random overlapping offsets; random init, MASK, and VERIFY against stored

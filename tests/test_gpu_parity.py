@@ -196,9 +196,10 @@ def test_huge_span_split_path(dev, oracle, route):
 
 
 @pytest.mark.parametrize("n", [1 << 18, (1 << 18) + 1, 300001])
-def test_pair_run_schedule(dev, oracle, native, n):
-    """Batches the pair-run span kernel takes (>= 2^18 spans, every span one
-    task): random lengths 0..4096 at random offsets, one in 997 a long span
+def test_pair_run_schedule(dev, oracle, native, n, bulk_route):
+    """Batches the pair-run span kernel takes on the planner path (>= 2^18
+    spans, every span one task), and the same batches as windows of the
+    one-launch kernel: random lengths 0..4096 at random offsets, one in 997 a long span
     (split path) instead, per-span init, Mask, VERIFY with every seventh
     trailer damaged; odd counts leave an odd last run."""
     import torch
@@ -274,7 +275,7 @@ def test_max_length_span(dev, oracle, native, route):
     torch.cuda.empty_cache()
 
 
-def test_segment_workspace_overflow_fallback(dev, oracle, native):
+def test_segment_workspace_overflow_fallback(dev, oracle, native, planner_bulk):
     """More long spans than the segment workspace lists (kCapLong = 2^18):
     the planner flags the overflow and the span pass folds every long span
     itself as a chain of 4 KiB chunks (no segment pass, no combine).  2^18 +
@@ -316,7 +317,7 @@ def test_segment_workspace_overflow_fallback(dev, oracle, native):
 
 
 @pytest.mark.parametrize("uniform", [False, True])
-def test_long_spans_close_slices(dev, oracle, uniform):
+def test_long_spans_close_slices(dev, oracle, uniform, bulk_route):
     """300 000 short spans with long (split-path) spans at positions 63 mod 64
     and elsewhere: a slice whose last record is a skipped long span must still
     store its other results (large batches, where a slice holds up to 64

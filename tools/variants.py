@@ -173,6 +173,11 @@ VARIANTS = {
             "    issue(tk[0], wb[0], eb[0]);\n    tables_wait<kRounds + 1>(tr);\n"),
            ("crc32c_direct.hip", "        issue(tk[3], wb[3], eb[3]);\n",
             "#pragma unroll\n        for (int q = 1; q < 4; ++q) issue(tk[q], wb[q], eb[q]);\n")],
+    # trailers as four byte stores (before round 4: one dword store)
+    "bytestores": [("crc32c_fold.h",
+                    '  asm volatile("global_store_dword %0, %1, off" : : "v"(p), "v"(v) : "memory");\n',
+                    "  uint8_t* q = const_cast<uint8_t*>(p);\n  q[0] = (uint8_t)v;\n  q[1] = (uint8_t)(v >> 8);\n"
+                    "  q[2] = (uint8_t)(v >> 16);\n  q[3] = (uint8_t)(v >> 24);\n")],
     # the table fill retired before any data load
     "t0": [("crc32c_direct.hip",
             "#pragma unroll\n    for (int q = 0; q < 3; ++q) issue(tk[q], wb[q], eb[q]);\n"
