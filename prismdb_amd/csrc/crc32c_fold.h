@@ -359,6 +359,15 @@ __device__ __forceinline__ void tables_issue(TableRegs<kT>& r, const DeviceTable
 
 // Retire the table loads with kYounger (data) loads left in flight.
 template <int kYounger>
+__device__ __forceinline__ void tables_wait(TableRegs<1024>& r) {
+  static_assert(TableRegs<1024>::kS == 8 && TableRegs<1024>::kN == 2, "operand list below");
+  asm volatile("s_waitcnt vmcnt(%10)"
+               : "+v"(r.v[0]), "+v"(r.v[1]), "+v"(r.v[2]), "+v"(r.v[3]), "+v"(r.v[4]), "+v"(r.v[5]),
+                 "+v"(r.v[6]), "+v"(r.v[7]), "+v"(r.u[0]), "+v"(r.u[1])
+               : "n"(kYounger));
+}
+
+template <int kYounger>
 __device__ __forceinline__ void tables_wait(TableRegs<768>& r) {
   static_assert(TableRegs<768>::kS == 11 && TableRegs<768>::kN == 3, "operand list below");
   asm volatile("s_waitcnt vmcnt(%14)"

@@ -173,6 +173,9 @@ VARIANTS = {
             "    issue(tk[0], wb[0], eb[0]);\n    tables_wait<kRounds + 1>(tr);\n"),
            ("crc32c_direct.hip", "        issue(tk[3], wb[3], eb[3]);\n",
             "#pragma unroll\n        for (int q = 1; q < 4; ++q) issue(tk[q], wb[q], eb[q]);\n")],
+    # the one-launch kernel at 16 waves per CU (1024-thread groups; needs
+    # <= 128 VGPRs): fewer tasks per wave, so a wave's chain of folds ends sooner
+    "w16": [("crc32c_device.h", "constexpr int kDirectThreads = 768;", "constexpr int kDirectThreads = 1024;")],
     # trailers as four byte stores (before round 4: one dword store)
     "bytestores": [("crc32c_fold.h",
                     '  asm volatile("global_store_dword %0, %1, off" : : "v"(p), "v"(v) : "memory");\n',
