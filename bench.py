@@ -448,6 +448,15 @@ def config5_leg(args, torch, dist, crc32c, dev, rank, world) -> dict:
     seal = leg(False, 1)
     verify = leg(True, 1)
     comp = {str(k): {"seal": leg(False, k), "verify": leg(True, k)} for k in kpcs}
+    from prismdb_amd._lib import lib as _native
+    for k in kpcs:
+        if k * spf > (1 << 17):  # more than one launch takes: the planner path (default) next to windows
+            prev = _native().prismdb_crc32c_windows(1)
+            try:
+                comp[str(k)]["seal_windows"] = leg(False, k)
+                comp[str(k)]["verify_windows"] = leg(True, k)
+            finally:
+                _native().prismdb_crc32c_windows(prev)
     torch.cuda.synchronize()
     bad = int(mm.sum().item())
     unmasked = (out.to(torch.int64) & 0xFFFFFFFF) - 0xA282EAD8

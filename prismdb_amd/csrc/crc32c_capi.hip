@@ -82,8 +82,13 @@ std::atomic<uint32_t> g_direct_cap{prismdb::dev::kDirectTickets};
 std::atomic<uint32_t> g_direct_dbg{0};
 // Descriptor batches of more than g_direct_max spans (without LOG_HEADER):
 // windows of the one-launch kernel on two side streams (1) or the planner
-// path (0).
-std::atomic<int> g_windows{1};
+// path (0, the default).  The one-launch kernel deals each wave a static run
+// of consecutive spans, and a group leaves its CU only when its slowest wave
+// is done: on spans of mixed sizes the windows lose to the planner's
+// task-balanced slices (config-3 mix 65.7 against 74.8 % of the roofline,
+// random spans 70.3 against 77.1 %), on uniform SST spans they win (72.8
+// against 70.8 %; profiles/r04/r04e_configs.json).
+std::atomic<int> g_windows{0};
 
 void BuildTables(DeviceTables* t) {
   namespace g = prismdb::gf2;
@@ -848,8 +853,8 @@ uint32_t prismdb_crc32c_direct_tickets(uint32_t cap) {
 uint32_t prismdb_crc32c_direct_debug(uint32_t flags) { return g_direct_dbg.exchange(flags, std::memory_order_relaxed); }
 
 // descriptor batches of more than prismdb_crc32c_direct_max spans (log-record
-// batches aside): 1 = windows of the one-launch kernel (default), 0 = the
-// planner path; returns the previous value.
+// batches aside): 1 = windows of the one-launch kernel, 0 = the planner path
+// (default); returns the previous value.
 int prismdb_crc32c_windows(int on) { return g_windows.exchange(on != 0 ? 1 : 0, std::memory_order_relaxed); }
 
 // the call count of the calling thread's workspace for (current device,

@@ -133,9 +133,10 @@ def native():
 
 
 # Descriptor-batch routes the GPU tests pin (C-ABI test hooks, not public):
-#   direct     the one-launch kernel (crc32c_direct.hip; the default: one
-#              launch for batches of <= 2^17 spans, windows of 2^17 spans on
-#              two side streams for larger ones -- log-record batches aside)
+#   direct     the one-launch kernel (crc32c_direct.hip; the default for
+#              batches of <= 2^17 spans) and, pinned here, windows of 2^17
+#              spans on two side streams for larger ones (log-record batches
+#              aside; the default for those is the planner path)
 #   windows    the one-launch kernel in windows of 1000 spans (many windows
 #              on modest batches)
 #   lane_log   the planner path, lane kernel in front of log-record batches
@@ -151,12 +152,12 @@ def set_route(native, name):
     direct_max, lane = ROUTES[name]
     native.prismdb_crc32c_direct_max(direct_max)
     native.prismdb_crc32c_lane_mode(lane)
-    native.prismdb_crc32c_windows(1)
+    native.prismdb_crc32c_windows(1 if name in ("direct", "windows") else 0)
 
     def restore():
         native.prismdb_crc32c_direct_max(1 << 17)
         native.prismdb_crc32c_lane_mode(0)
-        native.prismdb_crc32c_windows(1)
+        native.prismdb_crc32c_windows(0)
 
     return restore
 
@@ -179,8 +180,8 @@ def any_route(request, native):
 
 @pytest.fixture(params=["windows", "planner"])
 def bulk_route(request, native):
-    """Batches of more than 2^17 spans: windows of the one-launch kernel (the
-    default) and the planner path (windows off)."""
+    """Batches of more than 2^17 spans: windows of the one-launch kernel and
+    the planner path (the default)."""
     prev = native.prismdb_crc32c_windows(1 if request.param == "windows" else 0)
     yield request.param
     native.prismdb_crc32c_windows(prev)

@@ -721,8 +721,8 @@ def test_direct_random_batches(dev, oracle, native, seed):
 
 @pytest.mark.parametrize("mode", ["plain", "seal", "verify"])
 def test_bulk_windows_on_side_streams(dev, oracle, native, mode):
-    """A batch of 300 000 spans (> 2^17: windows of the one-launch kernel on
-    two side streams) on a caller stream that first uploads the bytes: the
+    """A batch of 300 000 spans (> 2^17) as windows of the one-launch kernel
+    on two side streams (the windows hook on) on a caller stream that first uploads the bytes: the
     windows start after the upload, the caller's stream waits for every
     window (results read there right after the call), and every result,
     trailer and verify flag equals the oracle's.  Lengths 0-8000 B at any
@@ -757,12 +757,16 @@ def test_bulk_windows_on_side_streams(dev, oracle, native, mode):
         d_init = torch.from_numpy(init.view(np.int32)).to(dev) if init is not None else None
         out = torch.full((n,), 7, dtype=torch.int32, device=dev)
         mm = torch.full((n,), 7, dtype=torch.uint8, device=dev)
-    if mode == "plain":
-        crc32c.batch(buf, d_off, d_len, d_init, out=out, stream=s, check_bounds=False)
-    elif mode == "seal":
-        crc32c.batch(buf, d_off, d_len, mask=True, trailer=True, out=out, stream=s, check_bounds=False)
-    else:
-        crc32c.batch(buf, d_off, d_len, verify=True, out=out, mismatch=mm, stream=s, check_bounds=False)
+    prev = native.prismdb_crc32c_windows(1)
+    try:
+        if mode == "plain":
+            crc32c.batch(buf, d_off, d_len, d_init, out=out, stream=s, check_bounds=False)
+        elif mode == "seal":
+            crc32c.batch(buf, d_off, d_len, mask=True, trailer=True, out=out, stream=s, check_bounds=False)
+        else:
+            crc32c.batch(buf, d_off, d_len, verify=True, out=out, mismatch=mm, stream=s, check_bounds=False)
+    finally:
+        native.prismdb_crc32c_windows(prev)
     with torch.cuda.stream(s):
         got, gmm, gbuf = out.clone(), mm.clone(), buf[:16].clone() if mode != "seal" else buf.clone()
     s.synchronize()

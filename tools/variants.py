@@ -164,6 +164,9 @@ VARIANTS = {
     # the one-launch kernel before round 4's ring change: two slots of three
     # streams (tools/patches/crc32c_direct_r03.hip, the round-3 source)
     "ring6": [("crc32c_direct.hip", "@file", "tools/patches/crc32c_direct_r03.hip")],
+    # two slots of two streams (positions mod 2): a fold waits for two tasks
+    # and runs two LDS chains (tools/patches/crc32c_direct_ring22.hip)
+    "ring22": [("crc32c_direct.hip", "@file", "tools/patches/crc32c_direct_ring22.hip")],
     # one task (17 loads) in flight before the table barrier instead of three:
     # the barrier then waits on fewer queued loads, the other three tasks go
     # out right after it
@@ -176,6 +179,11 @@ VARIANTS = {
     # the one-launch kernel at 16 waves per CU (1024-thread groups; needs
     # <= 128 VGPRs): fewer tasks per wave, so a wave's chain of folds ends sooner
     "w16": [("crc32c_device.h", "constexpr int kDirectThreads = 768;", "constexpr int kDirectThreads = 1024;")],
+    # measurement-only (trailers not written): the one-launch kernel sealing
+    # without its ring spans' trailer stores -- what they cost
+    "noseal": [("crc32c_direct.hip",
+                "        store_le32(reinterpret_cast<const uint8_t*>(hdr ? p - kLogCrcBack : body + gz + ((gf >> 12) & 3u)), res);\n",
+                "        (void)p;\n        (void)body;\n")] + MEASURE_ONLY,
     # trailers as four byte stores (before round 4: one dword store)
     "bytestores": [("crc32c_fold.h",
                     '  asm volatile("global_store_dword %0, %1, off" : : "v"(p), "v"(v) : "memory");\n',
@@ -307,7 +315,15 @@ def do_run(args, names):
     flen = torch.from_numpy(np.concatenate([np.full(nfd, 3988, dtype=np.int32), [486977]]).astype(np.int32)).to(dev)
     fout = torch.empty(nfd + 1, dtype=torch.int32, device=dev)
     fmm = torch.empty(nfd + 1, dtype=torch.uint8, device=dev)
-    calls = {"file_fixed": 50, "file_desc": 50, "file_seal": 50, "file_verify": 50, "tiny_desc": 50}
+    # seven such files in one call (the most one launch takes: 117 684 spans)
+    f7 = nfd * 3992 + 486977 + 4 + 3
+    f7off = torch.from_numpy(np.concatenate([np.arange(7, dtype=np.int64)[:, None] * f7 + np.concatenate(
+        [np.arange(nfd, dtype=np.int64) * 3992, [nfd * 3992]])[None, :]]).reshape(-1)).to(dev)
+    f7len = flen.repeat(7)
+    f7out = torch.empty(7 * (nfd + 1), dtype=torch.int32, device=dev)
+    f7mm = torch.empty(7 * (nfd + 1), dtype=torch.uint8, device=dev)
+    calls = {"file_fixed": 50, "file_desc": 50, "file_seal": 50, "file_verify": 50, "tiny_desc": 50,
+             "files7_seal": 10, "files7_verify": 10}
     work = {
         "fixed4k": (lambda n: libs[n][0](buf.data_ptr(), 4096, 4096, nblk, 0, out.data_ptr(), None, 0, sp),
                     nblk * 4100),
@@ -341,6 +357,11 @@ def do_run(args, names):
                                            fout.data_ptr(), None, 0x3, sp), nfd * (3988 + 16) + 486977 + 16),
         "file_verify": (lambda n: libs[n][1](buf.data_ptr(), foff.data_ptr(), flen.data_ptr(), None, nfd + 1,
                                              fout.data_ptr(), fmm.data_ptr(), 0, sp), nfd * (3988 + 17) + 486977 + 17),
+        "files7_seal": (lambda n: libs[n][1](buf.data_ptr(), f7off.data_ptr(), f7len.data_ptr(), None, 7 * (nfd + 1),
+                                             f7out.data_ptr(), None, 0x3, sp), 7 * (nfd * (3988 + 16) + 486977 + 16)),
+        "files7_verify": (lambda n: libs[n][1](buf.data_ptr(), f7off.data_ptr(), f7len.data_ptr(), None, 7 * (nfd + 1),
+                                               f7out.data_ptr(), f7mm.data_ptr(), 0, sp),
+                          7 * (nfd * (3988 + 17) + 486977 + 17)),
         # one span of 1 GiB - 3 B at an odd offset: the one-launch path's few-huge-spans case
         "one_huge": (lambda n: libs[n][1](buf.data_ptr(), hoff_.data_ptr(), h1len.data_ptr(), None, 1,
                                           hout.data_ptr(), None, 0, sp), (1 << 30) - 3 + 16),
@@ -364,7 +385,7 @@ def do_run(args, names):
     res = {w: {n: [] for n in names} for w in work}
     agree = {}
     outs_of = {"wal": wout, "wal_seal": wout, "sst3988": sout, "sst3988_seal": sout, "huge64m": hout, "one_huge": hout, "file_fixed": fout,
-               "file_desc": fout, "file_seal": fout,
+               "file_desc": fout, "file_seal": fout, "files7_seal": f7out, "files7_verify": f7out,
                "file_verify": fout, "tiny_desc": fout}
     for w, (fn, _) in work.items():
         ref = None
