@@ -164,6 +164,8 @@ VARIANTS = {
     # the one-launch kernel before round 4's ring change: two slots of three
     # streams (tools/patches/crc32c_direct_r03.hip, the round-3 source)
     "ring6": [("crc32c_direct.hip", "@file", "tools/patches/crc32c_direct_r03.hip")],
+    # round 4's first ring: one task sequence only, whatever the batch size
+    "ring4": [("crc32c_direct.hip", "@file", "tools/patches/crc32c_direct_ring4.hip")],
     # two slots of two streams (positions mod 2): a fold waits for two tasks
     # and runs two LDS chains (tools/patches/crc32c_direct_ring22.hip)
     "ring22": [("crc32c_direct.hip", "@file", "tools/patches/crc32c_direct_ring22.hip")],
@@ -320,10 +322,12 @@ def do_run(args, names):
     f7off = torch.from_numpy(np.concatenate([np.arange(7, dtype=np.int64)[:, None] * f7 + np.concatenate(
         [np.arange(nfd, dtype=np.int64) * 3992, [nfd * 3992]])[None, :]]).reshape(-1)).to(dev)
     f7len = flen.repeat(7)
+    f2n, f3n = 2 * (nfd + 1), 3 * (nfd + 1)  # two and three files: either side of the two-sequence limit
     f7out = torch.empty(7 * (nfd + 1), dtype=torch.int32, device=dev)
     f7mm = torch.empty(7 * (nfd + 1), dtype=torch.uint8, device=dev)
     calls = {"file_fixed": 50, "file_desc": 50, "file_seal": 50, "file_verify": 50, "tiny_desc": 50,
-             "files7_seal": 10, "files7_verify": 10}
+             "files7_seal": 10, "files7_verify": 10, "files2_seal": 20, "files2_verify": 20,
+             "files3_seal": 20, "files3_verify": 20}
     work = {
         "fixed4k": (lambda n: libs[n][0](buf.data_ptr(), 4096, 4096, nblk, 0, out.data_ptr(), None, 0, sp),
                     nblk * 4100),
@@ -362,6 +366,16 @@ def do_run(args, names):
         "files7_verify": (lambda n: libs[n][1](buf.data_ptr(), f7off.data_ptr(), f7len.data_ptr(), None, 7 * (nfd + 1),
                                                f7out.data_ptr(), f7mm.data_ptr(), 0, sp),
                           7 * (nfd * (3988 + 17) + 486977 + 17)),
+        "files2_seal": (lambda n: libs[n][1](buf.data_ptr(), f7off.data_ptr(), f7len.data_ptr(), None, f2n,
+                                             f7out.data_ptr(), None, 0x3, sp), 2 * (nfd * (3988 + 16) + 486977 + 16)),
+        "files2_verify": (lambda n: libs[n][1](buf.data_ptr(), f7off.data_ptr(), f7len.data_ptr(), None, f2n,
+                                               f7out.data_ptr(), f7mm.data_ptr(), 0, sp),
+                          2 * (nfd * (3988 + 17) + 486977 + 17)),
+        "files3_seal": (lambda n: libs[n][1](buf.data_ptr(), f7off.data_ptr(), f7len.data_ptr(), None, f3n,
+                                             f7out.data_ptr(), None, 0x3, sp), 3 * (nfd * (3988 + 16) + 486977 + 16)),
+        "files3_verify": (lambda n: libs[n][1](buf.data_ptr(), f7off.data_ptr(), f7len.data_ptr(), None, f3n,
+                                               f7out.data_ptr(), f7mm.data_ptr(), 0, sp),
+                          3 * (nfd * (3988 + 17) + 486977 + 17)),
         # one span of 1 GiB - 3 B at an odd offset: the one-launch path's few-huge-spans case
         "one_huge": (lambda n: libs[n][1](buf.data_ptr(), hoff_.data_ptr(), h1len.data_ptr(), None, 1,
                                           hout.data_ptr(), None, 0, sp), (1 << 30) - 3 + 16),
@@ -385,7 +399,8 @@ def do_run(args, names):
     res = {w: {n: [] for n in names} for w in work}
     agree = {}
     outs_of = {"wal": wout, "wal_seal": wout, "sst3988": sout, "sst3988_seal": sout, "huge64m": hout, "one_huge": hout, "file_fixed": fout,
-               "file_desc": fout, "file_seal": fout, "files7_seal": f7out, "files7_verify": f7out,
+               "file_desc": fout, "file_seal": fout, "files7_seal": f7out, "files7_verify": f7out, "files2_seal": f7out,
+               "files2_verify": f7out, "files3_seal": f7out, "files3_verify": f7out,
                "file_verify": fout, "tiny_desc": fout}
     for w, (fn, _) in work.items():
         ref = None
