@@ -24,8 +24,8 @@
 #include "crc32c_gf2.h"
 
 namespace prismdb {
-// Streams the engine creates for itself (pipeline rings, bulk-window side
-// streams, batch_multi cliques) carry their own workspace: defined below.
+// Streams the engine creates for itself (pipeline rings, batch_multi
+// cliques) carry their own workspace: defined below.
 void RegisterEngineStream(hipStream_t s);
 void ReleaseEngineStream(hipStream_t s);
 }  // namespace prismdb
@@ -81,8 +81,7 @@ std::atomic<uint64_t> g_direct_max{prismdb::dev::kDirectMaxSpans};
 std::atomic<uint32_t> g_direct_cap{prismdb::dev::kDirectTickets};
 std::atomic<uint32_t> g_direct_dbg{0};
 // Descriptor batches of more than g_direct_max spans (without LOG_HEADER):
-// windows of the one-launch kernel on two side streams (1) or the planner
-// path (0, the default).  The one-launch kernel deals each wave a static run
+// windows of the one-launch kernel (1) or the planner path (0, the default).  The one-launch kernel deals each wave a static run
 // of consecutive spans, and a group leaves its CU only when its slowest wave
 // is done: on spans of mixed sizes the windows lose to the planner's
 // task-balanced slices (config-3 mix 65.7 against 74.8 % of the roofline,
@@ -256,12 +255,6 @@ struct Workspace {
   char* direct = nullptr;  // word, done | ticket map | partials | per-span counters
   uint32_t gen = 0;
   SplitWs ws{};
-  // Bulk descriptor batches: windows of the one-launch kernel alternate
-  // between two side streams (each with its own workspace), forked from and
-  // joined back into this workspace's stream with events.
-  hipStream_t side[2] = {nullptr, nullptr};
-  hipEvent_t fork = nullptr;
-  hipEvent_t join[2] = {nullptr, nullptr};
 };
 
 // A thread that has used more streams than this evicts its least recently
@@ -289,15 +282,6 @@ void SyncAndRelease(Workspace& w) {
   if (hipDeviceGetDefaultMemPool(&pool, w.device) == hipSuccess) (void)hipMemPoolTrimTo(pool, 0);
   for (hipEvent_t ev : w.done)
     if (ev != nullptr) (void)hipEventDestroy(ev);
-  for (int k = 0; k < 2; ++k) {
-    if (w.side[k] != nullptr) {
-      (void)hipStreamSynchronize(w.side[k]);
-      prismdb::ReleaseEngineStream(w.side[k]);
-      (void)hipStreamDestroy(w.side[k]);
-    }
-    if (w.join[k] != nullptr) (void)hipEventDestroy(w.join[k]);
-  }
-  if (w.fork != nullptr) (void)hipEventDestroy(w.fork);
   if (w.device != cur) (void)hipSetDevice(cur);
   w = Workspace{};
 }
@@ -330,8 +314,8 @@ WorkspaceCache& ThreadWorkspaces() {
 }
 
 // Streams the engine itself owns and lends to one caller at a time (the host
-// pipeline's ring streams, leased from a per-device pool across threads; the
-// side streams of a workspace's bulk windows; batch_multi's clique streams):
+// pipeline's ring streams, leased from a per-device pool across threads;
+// batch_multi's clique streams):
 // their workspace belongs to the stream, not to the calling thread, and is
 // released with it (prismdb::ReleaseEngineStream) -- as thread-local entries
 // they piled up (up to kMaxWorkspaces per thread that ever leased a ring) or
@@ -507,47 +491,19 @@ int DirectWorkspace(Workspace& w, hipStream_t s, prismdb::dev::DirectWs* out) {
 enum Route { kRouteAuto = 0, kRouteDirect = 1, kRoutePlanner = 2 };
 
 // A descriptor batch of more spans than one launch of the one-launch kernel
-// takes, as ceil(n / wmax) equal windows of consecutive spans, each one
-// launch of that kernel.  Consecutive windows go to two side streams in
-// turn: a window's start-up (table fill, first round trip) then runs while
-// its predecessor drains instead of after it (on one stream the kernel
-// boundary cost ~12 us per window, profiles/r03s_chunked.json).  The side
-// streams start after everything already on s and s waits for both; each
-// side stream has its own workspace, so its windows alternate claim words
-// as any stream's calls do.
-int RunWindows(DeviceCtx& ctx, const SpanBatch& a, bool verify, hipStream_t s, Workspace& w, uint64_t wmax) {
-  hipError_t e = hipSuccess;
-  if (w.fork == nullptr) {
-    for (int k = 0; k < 2 && e == hipSuccess; ++k) {
-      e = hipStreamCreateWithFlags(&w.side[k], hipStreamNonBlocking);
-      if (e == hipSuccess) e = hipEventCreateWithFlags(&w.join[k], hipEventDisableTiming);
-    }
-    // (a side stream's workspace is the stream's, outside the thread's LRU:
-    // batch_multi's N devices x (clique stream + 2 side streams) would
-    // otherwise cycle through kMaxWorkspaces entries on every call)
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&w.fork, hipEventDisableTiming);
-    if (e == hipSuccess)
-      for (int k = 0; k < 2; ++k) prismdb::RegisterEngineStream(w.side[k]);
-    if (e != hipSuccess) {
-      for (int k = 0; k < 2; ++k) {
-        if (w.side[k] != nullptr) (void)hipStreamDestroy(w.side[k]);
-        if (w.join[k] != nullptr) (void)hipEventDestroy(w.join[k]);
-        w.side[k] = nullptr;
-        w.join[k] = nullptr;
-      }
-      w.fork = nullptr;
-      return FailHip(e, "side streams");
-    }
-  }
-  if ((e = hipEventRecord(w.fork, s)) != hipSuccess) return FailHip(e, "fork event");
-  for (int k = 0; k < 2; ++k)
-    if ((e = hipStreamWaitEvent(w.side[k], w.fork, 0)) != hipSuccess) return FailHip(e, "fork wait");
+// takes, as ceil(n / wmax) equal windows of consecutive spans, one launch of
+// that kernel each, back to back on the caller's stream.  (Round 4 first ran
+// the windows on two side streams so a window's start-up would overlap its
+// predecessor's tail; but the kernel's grid is one group per CU with static
+// runs dealt for every wave at once, and two such kernels in flight shared
+// the CUs: twelve SST files per call took 18.0 us per file that way against
+// 12.8 us in calls of seven files, profiles/r04/r04g_bench.json.)
+int RunWindows(DeviceCtx& ctx, const SpanBatch& a, bool verify, hipStream_t s, uint64_t wmax) {
   const uint64_t cap = 64ull * (uint64_t)ctx.cus * (prismdb::dev::kDirectThreads / 64);  // one span run per wave
   if (wmax > cap) wmax = cap;
   const uint64_t nwin = (a.n + wmax - 1) / wmax;
-  int rc = 0;
   uint64_t at = 0;
-  for (uint64_t k = 0; k < nwin && rc == 0; ++k) {
+  for (uint64_t k = 0; k < nwin; ++k) {
     const uint64_t m = (a.n - at) / (nwin - k);  // equal windows, the remainder spread over the last ones
     SpanBatch p = a;
     p.off += at;
@@ -556,19 +512,10 @@ int RunWindows(DeviceCtx& ctx, const SpanBatch& a, bool verify, hipStream_t s, W
     if (p.out != nullptr) p.out += at;
     if (p.mismatch != nullptr) p.mismatch += at;
     p.n = m;
-    rc = RunBatch(ctx, p, true, verify, w.side[k & 1u], kRouteDirect);
+    if (int rc = RunBatch(ctx, p, true, verify, s, kRouteDirect)) return rc;
     at += m;
   }
-  // joined whatever happened: s never runs ahead of work the call enqueued
-  for (int k = 0; k < 2; ++k) {
-    hipError_t j = hipEventRecord(w.join[k], w.side[k]);
-    if (j == hipSuccess) j = hipStreamWaitEvent(s, w.join[k], 0);
-    if (j != hipSuccess) {
-      (void)hipStreamSynchronize(w.side[k]);
-      if (rc == 0) rc = FailHip(j, "join");
-    }
-  }
-  return rc;
+  return 0;
 }
 
 // Launch sequence.  Fixed stride, aligned, <= 4 KiB: one kernel.  Descriptor
@@ -628,7 +575,7 @@ int RunBatch(DeviceCtx& ctx, const SpanBatch& base_args, bool desc, bool verify,
   const uint64_t wmax = g_direct_max.load(std::memory_order_relaxed);
   if (desc && route == kRouteAuto && wmax > 0 && a.n > wmax && g_windows.load(std::memory_order_relaxed) &&
       !(a.flags & prismdb::dev::kFlagLogHeader))
-    return RunWindows(ctx, base_args, verify, s, *w, wmax);
+    return RunWindows(ctx, base_args, verify, s, wmax);
   // The span kernel indexes records with 32 bits: cut larger batches.
   if (a.n > prismdb::dev::kMaxGenericSpans) {
     for (uint64_t i = 0; i < a.n; i += prismdb::dev::kMaxGenericSpans) {
@@ -725,8 +672,8 @@ int RunBatch(DeviceCtx& ctx, const SpanBatch& base_args, bool desc, bool verify,
 namespace prismdb {
 void SetLastError(const std::string& msg) { t_last_error = msg; }
 
-// The engine's own streams (pipeline rings, window side streams, clique
-// streams): one workspace per stream, whichever thread calls on it (one at
+// The engine's own streams (pipeline rings, clique streams): one workspace
+// per stream, whichever thread calls on it (one at
 // a time: a leased ring, the owning workspace's thread, the clique's mutex);
 // released (after its last batch) by ReleaseEngineStream before the stream
 // is destroyed.

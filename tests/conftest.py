@@ -135,8 +135,8 @@ def native():
 # Descriptor-batch routes the GPU tests pin (C-ABI test hooks, not public):
 #   direct     the one-launch kernel (crc32c_direct.hip; the default for
 #              batches of <= 2^17 spans) and, pinned here, windows of 2^17
-#              spans on two side streams for larger ones (log-record batches
-#              aside; the default for those is the planner path)
+#              spans back to back for larger ones (log-record batches aside;
+#              the default for those is the planner path)
 #   windows    the one-launch kernel in windows of 1000 spans (many windows
 #              on modest batches)
 #   lane_log   the planner path, lane kernel in front of log-record batches

@@ -720,11 +720,11 @@ def test_direct_random_batches(dev, oracle, native, seed):
 
 
 @pytest.mark.parametrize("mode", ["plain", "seal", "verify"])
-def test_bulk_windows_on_side_streams(dev, oracle, native, mode):
+def test_bulk_windows(dev, oracle, native, mode):
     """A batch of 300 000 spans (> 2^17) as windows of the one-launch kernel
-    on two side streams (the windows hook on) on a caller stream that first uploads the bytes: the
-    windows start after the upload, the caller's stream waits for every
-    window (results read there right after the call), and every result,
+    (the windows hook on), back to back on a caller stream that first
+    uploads the bytes: the windows start after the upload, the results are
+    read on that stream right after the call, and every result,
     trailer and verify flag equals the oracle's.  Lengths 0-8000 B at any
     alignment with random init, and 40 spans of 0.2-2 MiB (tickets)."""
     import torch

@@ -8,8 +8,8 @@ Prints one JSON object with, per workload, the mean kernel-sequence time
 of the algorithmic bytes (fixed L+4; variable L+4+12; verify
 L+4+1 per span):
   config3_mixed      spans of 1/4/16/64 KiB (uniform, seed 0x5EED0003) packed back to back, ~16 GiB
-  *_windows          the same batch as windows of 2^17 spans of the one-launch kernel on two side
-                     streams (the default for > 2^17 spans is the planner path)
+  *_windows          the same batch as windows of 2^17 spans of the one-launch kernel, back to back
+                     (the default for > 2^17 spans is the planner path)
   sst_fixed          3988-B spans (YCSB data block + type byte) at stride 3992, 16 Mi spans (~62.4 GiB)
   sst_desc           same spans through descriptors + one 486 977-B index span per 16 811 (split path)
   verify_4k          ReadBlock-verify of 16 Mi x (4092 + type... ) 4 KiB spans with stored trailers
