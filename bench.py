@@ -216,8 +216,10 @@ def cpu_baseline_leg(args, gpu_out, dev_buf) -> dict | None:
 def load_pmc_traffic(nblocks: int):
     """HBM bytes per launch of the span kernel from the committed PMC profile
     (profiles/*pmc*.json, written by tools/pmc_summary.py), if it matches."""
-    best = None
-    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
+    best = None  # the last match in path order: profiles/r04/... after profiles/r03...
+    paths = glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")) + \
+        glob.glob(os.path.join(ROOT, "profiles", "*", "*pmc*.json"))
+    for p in sorted(paths):
         try:
             with open(p) as f:
                 d = json.load(f)
