@@ -81,13 +81,19 @@ std::atomic<uint64_t> g_direct_max{prismdb::dev::kDirectMaxSpans};
 std::atomic<uint32_t> g_direct_cap{prismdb::dev::kDirectTickets};
 std::atomic<uint32_t> g_direct_dbg{0};
 // Descriptor batches of more than g_direct_max spans (without LOG_HEADER):
-// windows of the one-launch kernel (1) or the planner path (0, the default).  The one-launch kernel deals each wave a static run
+// windows of the one-launch kernel (1), the planner path (0), or (2, the
+// default) windows up to two of them and the planner path beyond.  Two
+// windows of SST files (twelve files, 201 744 spans) take 13.4 us per file,
+// against 21.6 on the planner path, whose 5-7 launches and segment pass cost
+// ~120 us per call; from there on the planner's balance wins, and on mixed
+// span sizes it wins at any size (profiles/r04/r04h_bench.json,
+// r04h_configs.json).  The one-launch kernel deals each wave a static run
 // of consecutive spans, and a group leaves its CU only when its slowest wave
 // is done: on spans of mixed sizes the windows lose to the planner's
 // task-balanced slices (config-3 mix 65.7 against 74.8 % of the roofline,
 // random spans 70.3 against 77.1 %), on uniform SST spans they win (72.8
 // against 70.8 %; profiles/r04/r04e_configs.json).
-std::atomic<int> g_windows{0};
+std::atomic<int> g_windows{2};
 // The planner path's span pass for batches that are not log records: one
 // task sequence per wave (1, crc32c_span1_kernel) or round 3's two streams
 // per wave with pair runs (0).
@@ -254,6 +260,7 @@ struct Workspace {
   void* mem = nullptr;
   char* grow = nullptr;
   size_t cap_rec = 0;
+  uint32_t cap_streams = 0;  // the span-kernel streams the slice starts of `grow` were sized for
   char* qgrow = nullptr;
   size_t cap_q = 0;
   char* direct = nullptr;  // word, done | ticket map | partials | per-span counters
@@ -421,10 +428,15 @@ int GrowBlock(char** blk, size_t bytes, hipStream_t s, const char* what) {
 }
 
 int PlannerWorkspace(Workspace& w, hipStream_t s, size_t nspans, uint32_t streams, bool lane, SplitWs* out) {
-  if (w.cap_rec < nspans) {
+  // The slice starts' room depends on the stream count too (one or two
+  // streams per wave): a block sized for fewer streams is grown, and the
+  // layout below follows the block's own sizing, never the call's.
+  if (w.cap_rec < nspans || w.cap_streams < streams) {
     const size_t cap = nspans < 4096 ? 4096 : nspans + nspans / 4;
-    const size_t bytes = cap * (16 + 4) + SliceCap(cap, streams) * 8 + 16;
+    const uint32_t cs = streams > w.cap_streams ? streams : w.cap_streams;
+    const size_t bytes = cap * (16 + 4) + SliceCap(cap, cs) * 8 + 16;
     w.cap_rec = 0;
+    w.cap_streams = cs;
     if (int rc = GrowBlock(&w.grow, bytes, s, "span record workspace")) return rc;
     w.cap_rec = cap;
   }
@@ -440,7 +452,7 @@ int PlannerWorkspace(Workspace& w, hipStream_t s, size_t nspans, uint32_t stream
   w.ws.qrun = lane ? reinterpret_cast<uint8_t*>(w.qgrow + w.cap_q * 9) : nullptr;
   w.ws.rec = reinterpret_cast<prismdb::dev::SpanRec*>(w.grow);
   w.ws.slice_start = reinterpret_cast<uint64_t*>(w.grow + w.cap_rec * 16);
-  w.ws.cnt = reinterpret_cast<uint32_t*>(w.grow + w.cap_rec * 16 + SliceCap(w.cap_rec, streams) * 8);
+  w.ws.cnt = reinterpret_cast<uint32_t*>(w.grow + w.cap_rec * 16 + SliceCap(w.cap_rec, w.cap_streams) * 8);
   // Planner tiles: whole multiples of its block size, at most kMaxPlanBlocks.
   namespace d = prismdb::dev;
   const uint64_t per = (nspans + d::kMaxPlanBlocks - 1) / d::kMaxPlanBlocks;
@@ -577,7 +589,8 @@ int RunBatch(DeviceCtx& ctx, const SpanBatch& base_args, bool desc, bool verify,
   }
   // Bulk descriptor batches: windows of the one-launch kernel.
   const uint64_t wmax = g_direct_max.load(std::memory_order_relaxed);
-  if (desc && route == kRouteAuto && wmax > 0 && a.n > wmax && g_windows.load(std::memory_order_relaxed) &&
+  const int wmode = g_windows.load(std::memory_order_relaxed);
+  if (desc && route == kRouteAuto && wmax > 0 && a.n > wmax && (wmode == 1 || (wmode == 2 && a.n <= 2 * wmax)) &&
       !(a.flags & prismdb::dev::kFlagLogHeader))
     return RunWindows(ctx, base_args, verify, s, wmax);
   // The span kernel indexes records with 32 bits: cut larger batches.
@@ -808,9 +821,12 @@ uint32_t prismdb_crc32c_direct_tickets(uint32_t cap) {
 uint32_t prismdb_crc32c_direct_debug(uint32_t flags) { return g_direct_dbg.exchange(flags, std::memory_order_relaxed); }
 
 // descriptor batches of more than prismdb_crc32c_direct_max spans (log-record
-// batches aside): 1 = windows of the one-launch kernel, 0 = the planner path
-// (default); returns the previous value.
-int prismdb_crc32c_windows(int on) { return g_windows.exchange(on != 0 ? 1 : 0, std::memory_order_relaxed); }
+// batches aside): 1 = windows of the one-launch kernel, 0 = the planner path,
+// 2 = windows up to two of them, the planner beyond (default); returns the
+// previous value.
+int prismdb_crc32c_windows(int mode) {
+  return g_windows.exchange(mode < 0 || mode > 2 ? 2 : mode, std::memory_order_relaxed);
+}
 
 // the planner path's span pass for batches that are not log records: 1 = one
 // task sequence per wave (default), 0 = two streams per wave (round 3's

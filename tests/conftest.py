@@ -136,7 +136,7 @@ def native():
 #   direct     the one-launch kernel (crc32c_direct.hip; the default for
 #              batches of <= 2^17 spans) and, pinned here, windows of 2^17
 #              spans back to back for larger ones (log-record batches aside;
-#              the default for those is the planner path)
+#              the default: windows up to 2^18 spans, the planner beyond)
 #   windows    the one-launch kernel in windows of 1000 spans (many windows
 #              on modest batches)
 #   lane_log   the planner path, lane kernel in front of log-record batches
@@ -157,7 +157,7 @@ def set_route(native, name):
     def restore():
         native.prismdb_crc32c_direct_max(1 << 17)
         native.prismdb_crc32c_lane_mode(0)
-        native.prismdb_crc32c_windows(0)
+        native.prismdb_crc32c_windows(2)
 
     return restore
 
@@ -181,7 +181,7 @@ def any_route(request, native):
 @pytest.fixture(params=["windows", "planner"])
 def bulk_route(request, native):
     """Batches of more than 2^17 spans: windows of the one-launch kernel and
-    the planner path (the default)."""
+    the planner path (the default picks windows up to 2^18 spans)."""
     prev = native.prismdb_crc32c_windows(1 if request.param == "windows" else 0)
     yield request.param
     native.prismdb_crc32c_windows(prev)

@@ -843,3 +843,39 @@ def test_short_records_far_apart(dev, oracle, short_route):
     np.testing.assert_array_equal(_u32(out), want)
     del buf
     torch.cuda.empty_cache()
+
+
+def test_planner_workspace_across_stream_counts(dev, oracle, native):
+    """One caller stream, three planner-path batches in a row: spans that are
+    not log records (the one-sequence span kernel: slices planned for one
+    stream per wave), then log records (the two-stream kernel: twice the
+    slice starts), then the first batch again.  The workspace's slice-start
+    room follows the larger stream count (round 4's first build laid the
+    second batch out past the block sized by the first: an illegal address
+    in smoke()).  Every result against the oracle."""
+    import torch
+    from prismdb_amd import crc32c
+    from conftest import set_route
+
+    rng = np.random.default_rng(0x5EED0090)
+    n = 3000
+    lens = rng.integers(1, 1200, size=n).astype(np.uint32)
+    off = (np.cumsum(lens.astype(np.uint64) + 11) - lens.astype(np.uint64) + 7).astype(np.uint64)
+    host = oracle.synth(int(off[-1]) + int(lens[-1]) + 64, 0x5EED0091)
+    want, _ = oracle.batch(host, off, lens)
+    s = torch.cuda.Stream(dev)
+    restore = set_route(native, "lane_log")  # the planner path for every size
+    try:
+        with torch.cuda.stream(s):
+            buf = torch.from_numpy(host).to(dev)
+            d_off = torch.from_numpy(off.astype(np.int64)).to(dev)
+            d_len = torch.from_numpy(lens.view(np.int32)).to(dev)
+        outs = []
+        for log_header in (False, True, False):
+            o, _ = crc32c.batch(buf, d_off, d_len, log_header=log_header, stream=s, check_bounds=False)
+            outs.append(o)
+        s.synchronize()
+    finally:
+        restore()
+    for o in outs:
+        np.testing.assert_array_equal(_u32(o), want)
