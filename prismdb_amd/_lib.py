@@ -76,7 +76,6 @@ def _declare(lib: ctypes.CDLL) -> None:
         "prismdb_crc32c_direct_set_gen": (ctypes.c_int, [vp, u32]),
         "prismdb_crc32c_multi_fail_after": (ctypes.c_int, [ctypes.c_int]),
         "prismdb_crc32c_windows": (ctypes.c_int, [ctypes.c_int]),
-        "prismdb_crc32c_span1": (ctypes.c_int, [ctypes.c_int]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

@@ -846,13 +846,14 @@ def test_short_records_far_apart(dev, oracle, short_route):
 
 
 def test_planner_workspace_across_stream_counts(dev, oracle, native):
-    """One caller stream, three planner-path batches in a row: spans that are
-    not log records (the one-sequence span kernel: slices planned for one
-    stream per wave), then log records (the two-stream kernel: twice the
-    slice starts), then the first batch again.  The workspace's slice-start
-    room follows the larger stream count (round 4's first build laid the
-    second batch out past the block sized by the first: an illegal address
-    in smoke()).  Every result against the oracle."""
+    """One caller stream, three planner-path batches in a row reusing one
+    workspace: spans that are not log records, then the same spans as log
+    records (the lane kernel and its list in front), then the first batch
+    again.  Round 4 once planned the first kind for half the span-kernel
+    streams, and the second laid its slice starts out past the block the
+    first had sized (an illegal address in smoke()): the workspace now
+    follows the largest stream count it served.  Every result against the
+    oracle."""
     import torch
     from prismdb_amd import crc32c
     from conftest import set_route

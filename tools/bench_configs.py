@@ -8,8 +8,6 @@ Prints one JSON object with, per workload, the mean kernel-sequence time
 of the algorithmic bytes (fixed L+4; variable L+4+12; verify
 L+4+1 per span):
   config3_mixed      spans of 1/4/16/64 KiB (uniform, seed 0x5EED0003) packed back to back, ~16 GiB
-  *_span2            the same batch through round 3's two-stream span kernel (the default since
-                     round 4 is one task sequence per wave, crc32c_span1_kernel)
   *_windows          the same batch as windows of 2^17 spans of the one-launch kernel, back to back
                      (the default for > 2^17 spans is the planner path)
   sst_fixed          3988-B spans (YCSB data block + type byte) at stride 3992, 16 Mi spans (~62.4 GiB)
@@ -70,15 +68,6 @@ def main():
                 native().prismdb_crc32c_windows(prev)
         return run
 
-    def span2(fn):  # the planner path with round 3's two-stream span kernel (pair runs)
-        def run():
-            prev = native().prismdb_crc32c_span1(0)
-            try:
-                fn()
-            finally:
-                native().prismdb_crc32c_span1(prev)
-        return run
-
     def report(name, t, payload, algo, n):
         res[name] = {"spans": n, "payload_GiB": round(payload / GIB, 2), "ms": round(t * 1e3, 3),
                      "GiB/s": round(payload / t / GIB, 1), "algo_GB/s": round(algo / t / 1e9, 1),
@@ -101,8 +90,6 @@ def main():
         report("config3_mixed_windows", timed(windows(fn), args.reps), lens.sum(), lens.sum() + 16 * len(lens),
                len(lens))
         res["config3_mixed_windows"]["agrees"] = bool(torch.equal(ref, out))
-        report("config3_mixed_span2", timed(span2(fn), args.reps), lens.sum(), lens.sum() + 16 * len(lens), len(lens))
-        res["config3_mixed_span2"]["agrees"] = bool(torch.equal(ref, out))
         del d_off, d_len, out
 
     # SST-shaped, fixed stride
@@ -136,8 +123,6 @@ def main():
         ref = out2.clone()
         report("sst_desc_windows", timed(windows(fn), args.reps), lens.sum(), lens.sum() + 16 * len(lens), len(lens))
         res["sst_desc_windows"]["agrees"] = bool(torch.equal(ref, out2))
-        report("sst_desc_span2", timed(span2(fn), args.reps), lens.sum(), lens.sum() + 16 * len(lens), len(lens))
-        res["sst_desc_span2"]["agrees"] = bool(torch.equal(ref, out2))
         del d_off, d_len, out2
 
     # verify 4 KiB spans (fixed stride 4096, span 4092 B, trailer in the last 4 B)
@@ -159,8 +144,6 @@ def main():
         ref = out3.clone()
         report("adversarial_windows", timed(windows(fn), args.reps), lens.sum(), lens.sum() + 16 * m, m)
         res["adversarial_windows"]["agrees"] = bool(torch.equal(ref, out3))
-        report("adversarial_span2", timed(span2(fn), args.reps), lens.sum(), lens.sum() + 16 * m, m)
-        res["adversarial_span2"]["agrees"] = bool(torch.equal(ref, out3))
 
         del d_off, d_len, out3
 

@@ -94,6 +94,10 @@ std::atomic<uint32_t> g_direct_dbg{0};
 // random spans 70.3 against 77.1 %), on uniform SST spans they win (72.8
 // against 70.8 %; profiles/r04/r04e_configs.json).
 std::atomic<int> g_windows{2};
+// The planner path's span pass for batches that are not log records: one
+// task sequence per wave (1, crc32c_span1_kernel) or round 3's two streams
+// per wave with pair runs (0).
+std::atomic<int> g_span1{1};
 
 void BuildTables(DeviceTables* t) {
   namespace g = prismdb::gf2;
@@ -424,10 +428,9 @@ int GrowBlock(char** blk, size_t bytes, hipStream_t s, const char* what) {
 }
 
 int PlannerWorkspace(Workspace& w, hipStream_t s, size_t nspans, uint32_t streams, bool lane, SplitWs* out) {
-  // The slice starts' room depends on the stream count too: a block sized
-  // for fewer streams is grown, and the layout below follows the block's own
-  // sizing, never the call's (round 4's one-sequence span kernel, planned
-  // for half the streams, overran it).
+  // The slice starts' room depends on the stream count too (one or two
+  // streams per wave): a block sized for fewer streams is grown, and the
+  // layout below follows the block's own sizing, never the call's.
   if (w.cap_rec < nspans || w.cap_streams < streams) {
     const size_t cap = nspans < 4096 ? 4096 : nspans + nspans / 4;
     const uint32_t cs = streams > w.cap_streams ? streams : w.cap_streams;
@@ -613,11 +616,12 @@ int RunBatch(DeviceCtx& ctx, const SpanBatch& base_args, bool desc, bool verify,
   // below then runs over the list of the others only.
   const int lane_mode = g_lane_mode.load(std::memory_order_relaxed);
   const bool lane = desc && (lane_mode > 0 || (lane_mode == 0 && (a.flags & prismdb::dev::kFlagLogHeader)));
-  // The span kernel's record streams: two per wave of its persistent grid.
-  // (Round 4 tried one task sequence per wave here, the one-launch kernel's
-  // ring: within +-2 % on the bulk rows, profiles/r04/r04i_configs_*.json;
-  // its sources are tools/patches/span1/.)
-  const uint32_t streams = 2u * (uint32_t)ctx.cus * prismdb::dev::kWavesPerGroup;
+  // The span pass: one task sequence per wave (crc32c_span1_kernel) for
+  // everything but log records, which keep the two-stream kernel that skips
+  // their padding rounds (and the lane kernel's list).  The slices are
+  // planned for its record streams: one per wave, or two.
+  const bool one = !lane && !(a.flags & prismdb::dev::kFlagLogHeader) && g_span1.load(std::memory_order_relaxed);
+  const uint32_t streams = (one ? 1u : 2u) * (uint32_t)ctx.cus * prismdb::dev::kWavesPerGroup;
   if ((rc = PlannerWorkspace(*w, s, a.n, streams, lane, &ws)) != 0) return rc;
   hipError_t e = hipMemsetAsync(ws.counters, 0, sizeof(SplitCounters), s);
   if (e != hipSuccess) return FailHip(e, "hipMemsetAsync");
@@ -654,11 +658,11 @@ int RunBatch(DeviceCtx& ctx, const SpanBatch& base_args, bool desc, bool verify,
   // Large batches of one-task records take the pair-run kernel (its two
   // streams read adjacent spans); it is launched next to the general one,
   // and the one whose schedule the scan did not pick leaves at once.
-  a.pair_kernel = a.slice_start != nullptr && a.n >= prismdb::dev::kPairMinSpans && !lane &&
+  a.pair_kernel = !one && a.slice_start != nullptr && a.n >= prismdb::dev::kPairMinSpans && !lane &&
                           !(a.flags & prismdb::dev::kFlagLogHeader)
                       ? 1u
                       : 0u;
-  e = prismdb::dev::launch_span(a, verify, ctx.cus, s);
+  e = one ? prismdb::dev::launch_span1(a, verify, ctx.cus, s) : prismdb::dev::launch_span(a, verify, ctx.cus, s);
   if (e != hipSuccess) return FailHip(e, "span kernel launch");
   SpanBatch seg{};
   seg.base = a.base;
@@ -823,6 +827,11 @@ uint32_t prismdb_crc32c_direct_debug(uint32_t flags) { return g_direct_dbg.excha
 int prismdb_crc32c_windows(int mode) {
   return g_windows.exchange(mode < 0 || mode > 2 ? 2 : mode, std::memory_order_relaxed);
 }
+
+// the planner path's span pass for batches that are not log records: 1 = one
+// task sequence per wave (default), 0 = two streams per wave (round 3's
+// kernel, pair runs); returns the previous value.
+int prismdb_crc32c_span1(int on) { return g_span1.exchange(on != 0 ? 1 : 0, std::memory_order_relaxed); }
 
 // the call count of the calling thread's workspace for (current device,
 // stream): the next one-launch call there takes gen + 1 (its tag: the low 16

@@ -177,6 +177,9 @@ constexpr uint64_t kMaxGenericSpans = 1ull << 30;  // per generic-path launch se
 constexpr uint32_t kPlanThreads = 256;
 
 hipError_t launch_span(const SpanBatch& a, bool verify, int grid, hipStream_t s);
+// one task sequence per wave (span role, not log records): slices planned for
+// one stream per wave (SplitWs::nstreams = waves)
+hipError_t launch_span1(const SpanBatch& a, bool verify, int grid, hipStream_t s);
 hipError_t launch_fixed(const SpanBatch& a, bool verify, int grid, hipStream_t s);
 hipError_t launch_plan(const SpanBatch& a, bool desc, const SplitWs& ws, hipStream_t s);
 hipError_t launch_slices(const SpanBatch& a, const SplitWs& ws, hipStream_t s);

@@ -487,6 +487,245 @@ drained:
 }
 
 // ---------------------------------------------------------------------------
+// Record-driven span kernel with ONE task sequence per wave (round 4; the
+// default for descriptor batches that are not log records; the kernel above
+// keeps the log-record batches and the segment pass).  The wave's stream
+// takes slices (or runs) w, w + S, ... (S = nwaves: the host plans the slices
+// for one stream per wave), a span's chunks one after another, through a
+// ring of four single-task slots: the wave waits for its oldest task only
+// (the three younger tasks' 51 loads stay in flight) and folds it as one LDS
+// chain as soon as it has landed, the 16 waves of a CU interleaving their
+// chains -- the one-launch kernel's ring (crc32c_direct.hip), which beat two
+// slots of three streams there by 3-10 %.  Records come through the scalar
+// cache one span ahead, every task issues exactly 17 loads (16 body dwords +
+// 1 edge byte; range-checked buffer loads give chunk 0 its zero padding and
+// let invalid or skipped tasks run the same code).
+// ---------------------------------------------------------------------------
+template <bool kVerify>
+__global__ __launch_bounds__(kThreads) void crc32c_span1_kernel(SpanBatch a) {
+  constexpr int kR = kRounds;
+  constexpr uint32_t kLgC = 10u;        // log2(chunk words): 4 KiB chunks
+  constexpr uint32_t kLgB = kLgC + 2u;  // log2(chunk bytes)
+  uint32_t n = (uint32_t)a.n;           // (the host cuts generic batches at kMaxGenericSpans)
+  if (a.n_dev != nullptr) {
+    const uint64_t m = *a.n_dev;
+    n = m < n ? (uint32_t)m : n;
+  }
+  const bool hdr = (a.flags & kFlagLogHeader) != 0;
+  bool skip_long = true;  // long spans go through segments...
+  if (a.overflow != nullptr && *a.overflow != 0u) skip_long = false;  // ...unless that workspace overflowed
+  if (n == 0) return;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t lane = tid & 63u;
+  const uint32_t wave = rfl(blockIdx.x * kWavesPerGroup + (tid >> 6));
+  const uint32_t nwaves = gridDim.x * kWavesPerGroup;
+  // Schedule: stream = wave, S = nwaves.  Task-balanced slices when the scan
+  // made them (slice k = records [slice_start[k], slice_start[k+1]), <= 64),
+  // else runs of q or q+1 records, exactly m per stream (m >= kRunsPerStream
+  // while runs keep >= 1 record).
+  const uint32_t S = nwaves;
+  bool sliced = a.slice_start != nullptr;
+  uint32_t K = sliced ? (uint32_t)const_load(a.nslices_dev, 0) : 0u;
+  uint32_t rq = 0, rr = 0;
+  if (K == 0) {
+    sliced = false;
+    uint32_t m = (uint32_t)(((uint64_t)n + 63ull * S - 1u) / (63ull * S));
+    if (m < kRunsPerStream) {
+      const uint32_t mr = n / S;
+      m = mr < kRunsPerStream ? (mr > m ? mr : m) : kRunsPerStream;
+    }
+    if (m < 1u) m = 1u;
+    K = (uint64_t)m * S < n ? m * S : n;
+    rq = n / K;
+    rr = n % K;
+  }
+  // a group whose waves all have no slice or run leaves before the table fill
+  if (blockIdx.x * kWavesPerGroup >= K) return;
+
+  __shared__ uint32_t lds[kLdsWords];
+  load_tables(lds, a.tabs, tid);
+  __syncthreads();
+  const StrideLanes tab = stride_lanes(lane);
+  const uint32_t nibtab = 4u * (kTabWords + lane);
+  const ShortShift ss = short_shift_cols(lane);
+  struct Cursor {
+    uint32_t b, lo, hi, k;
+  };
+  Cursor cur;
+  // first slice or run >= k with a record
+  auto open = [&](uint32_t k) {
+    for (; k < K; k += S) {
+      uint32_t lo, hi;
+      if (sliced) {
+        lo = (uint32_t)const_load(a.slice_start, k);
+        hi = (uint32_t)const_load(a.slice_start, k + 1);
+      } else {
+        lo = k * rq + (k < rr ? k : rr);
+        hi = lo + rq + (k < rr ? 1u : 0u);
+      }
+      hi = hi < n ? hi : n;
+      if (lo < hi) {
+        cur.b = lo;
+        cur.lo = lo;
+        cur.hi = hi;
+        cur.k = k;
+        return;
+      }
+    }
+    cur.b = cur.lo = cur.hi = n;
+    cur.k = K;
+  };
+  auto advance = [&]() {
+    if (cur.b + 1u < cur.hi) cur.b += 1u;
+    else open(cur.k + S);
+  };
+  auto read_rec = [&](uint32_t b) -> SpanRec {
+    SpanRec r{0u, 0u, 0u, 0u};
+    if (b < n) r = const_load(a.rec, b);
+    return r;
+  };
+  SpanRec pend;  // the record of the stream's next span
+  // The task after t (the newest one): t's next chunk, or chunk 0 of the
+  // pending record (then the record after it is requested).
+  auto next_task = [&](const Task& t) -> Task {
+    if (t.valid() && !t.skip() && t.c + 1 < t.nch(kLgB)) {  // a skipped (long) span is one task
+      Task u = t;
+      u.c = t.c + 1;
+      return u;
+    }
+    Task u;
+    u.b = cur.b;
+    u.r = pend;
+    u.c = 0;
+    const bool valid = cur.b < n;
+    const bool skip = !valid || (skip_long && u.lng());
+    u.f = (cur.b - cur.lo) | (cur.b + 1u >= cur.hi ? 1u << 8 : 0u) | (valid ? 1u << 9 : 0u) | (skip ? 1u << 10 : 0u);
+    if (valid) {
+      advance();
+      pend = read_rec(cur.b);
+    }
+    return u;
+  };
+  // 17 loads, always (crc32c_span_kernel's issue, without the log window).
+  auto issue = [&](const Task& t, uint32_t (&w)[kR], uint32_t& e) {
+    const bool live = !t.skip();
+    const uint32_t pad = t.pad(), tl = t.t(), nch = t.nch(kLgB), len = t.len();
+    const bool hwin = kVerify && hdr;
+    auto sat = [](uint64_t x) -> uint32_t { return x > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)x; };
+    u32x4 rb = buffer_rsrc(t.body(), live ? t.r.z : 0u);
+    u32x4 re = buffer_rsrc(hwin ? t.start() - kLogCrcBack : t.body() + t.r.z,
+                           live ? (hwin ? sat((uint64_t)kLogCrcBack + len) : tl + (kVerify ? 4u : 0u)) : 0u);
+    // (descriptors from uniform record fields on the scalar unit only: no
+    // VALU-written SGPR reaches the asm loads, tools/check_asm_hazards.py)
+    asm volatile("" : "+s"(rb), "+s"(re));
+    const int32_t i0 = (int32_t)((t.c << kLgC) + lane) - (int32_t)pad;
+    if (t.c != 0 || pad == 0) {
+      load_rounds(w, rb, (uint32_t)i0 * 4u);
+    } else if (pad <= 64u) {
+      w[0] = buf_dword<0>(rb, (uint32_t)i0 * 4u);
+      load_rounds_from1(w, rb, (uint32_t)(i0 + 64) * 4u);
+    } else {
+#pragma unroll
+      for (int j = 0; j < kR; ++j) w[j] = buf_dword<0>(rb, (uint32_t)(i0 + 64 * j) * 4u);
+    }
+    const bool last = t.c + 1 == nch;
+    uint32_t eoff = 0xFFFFFFFFu;
+    if (last && lane >= 3u && lane < 3u + tl)
+      eoff = hwin ? sat((uint64_t)kLogCrcBack + t.h() + t.r.z + (lane - 3u)) : lane - 3u;
+    if (kVerify && last && lane >= 6u && lane < 10u) eoff = (hwin ? 0u : tl) + (lane - 6u);
+    e = buf_ubyte(re, eoff);
+  };
+
+  uint32_t acc = 0u, reg = 0u;  // the chain, and the span's initial register (chunk 0)
+  uint32_t res = 0u, bad = 0u;  // the slice's results: lane i = record lo + i
+  auto flush = [&](const Task& t) {
+    const uint32_t lo = t.b - t.slot();
+    if (lane <= t.slot()) {
+      if (a.out != nullptr) __builtin_nontemporal_store(res, a.out + lo + lane);
+      if (kVerify && a.mismatch != nullptr) __builtin_nontemporal_store((uint8_t)bad, a.mismatch + lo + lane);
+    }
+  };
+  auto finish = [&](const Task& t, uint32_t e, uint32_t body) {
+    const uint32_t tl = t.t();
+    const uint32_t d = tl ? readlane(e, 3) | (readlane(e, 4) << 8) | (readlane(e, 5) << 16) : 0u;
+    const uint32_t crc = feed_short(ss, lane, t.r.z ? body : reg, d, tl) ^ kConditioning;
+    const uint32_t v = (a.flags & kFlagMask) ? mask_crc(crc) : crc;
+    const uint32_t slot = t.slot();
+    res = lane == slot ? v : res;
+    if (kVerify) {
+      const uint32_t stored = readlane(e, 6) | (readlane(e, 7) << 8) | (readlane(e, 8) << 16) | (readlane(e, 9) << 24);
+      bad = lane == slot ? (crc != unmask_crc(stored) ? 1u : 0u) : bad;
+    }
+    if ((a.flags & kFlagWriteTrailer) && lane == 0)
+      store_le32(hdr ? t.start() - kLogCrcBack : t.body() + t.r.z + tl, v);
+    if (t.last()) flush(t);
+  };
+  // One task: chunk 0 starts the chain from the span's initial register
+  // (already fed the head bytes by the planner), which enters with body word
+  // 0 (lane pad % 64 of round pad / 64, a masked XOR per round when that
+  // round is not the first); the span's last chunk finishes it.
+  auto fold = [&](const Task& t, uint32_t (&w)[kR], uint32_t e) {
+    if (!t.skip() && t.c == 0) {
+      reg = t.r.w;
+      acc = 0u;
+      if (t.r.z != 0) {
+        const uint32_t pad = t.pad();
+        const uint32_t J = pad >> 6;
+        const uint32_t inj = lane == (pad & 63u) ? reg : 0u;
+        if (J == 0) {
+          w[0] ^= inj;
+        } else {
+#pragma unroll
+          for (int j = 1; j < kR; ++j)
+            w[j] = __builtin_amdgcn_bitop3_b32(w[j], inj, (uint32_t)j == J ? ~0u : 0u, 0x78);
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < kR; ++j) acc = step256(lds, tab, acc, w[j]);
+    if (!t.skip() && t.c + 1 == t.nch(kLgB)) finish(t, e, wave_xor(realign(lds, nibtab, acc)));
+    // a skipped long span's result comes from the combine pass, but it may
+    // close its slice: the slice's other results are stored now
+    if (t.skip() && t.valid() && t.last()) flush(t);
+  };
+
+  Task tk[4];
+  uint32_t wb[4][kR];
+  uint32_t eb[4];
+  open(wave);
+  {
+    Task none;
+    none.b = n;
+    none.r = SpanRec{0u, 0u, 0u, 0u};
+    none.c = 0;
+    none.f = 0;  // invalid: next_task takes the first record
+    pend = read_rec(cur.b);
+    tk[0] = next_task(none);
+  }
+  if (!tk[0].valid()) return;
+  tk[1] = next_task(tk[0]);
+  tk[2] = next_task(tk[1]);
+  tk[3] = next_task(tk[2]);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) issue(tk[q], wb[q], eb[q]);
+  constexpr int kYounger = 3 * (kR + 1);  // the three younger tasks
+  for (;;) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      wait_task<kYounger>(wb[q], eb[q]);
+      if (tk[q].valid()) fold(tk[q], wb[q], eb[q]);
+      // tasks are made in sequence: the next one invalid, all are
+      if (!tk[(q + 1) & 3].valid()) goto drained;
+      tk[q] = next_task(tk[(q + 3) & 3]);
+      issue(tk[q], wb[q], eb[q]);
+    }
+  }
+drained:
+#pragma unroll
+  for (int q = 0; q < 4; ++q) wait_task<0>(wb[q], eb[q]);
+}
+
+// ---------------------------------------------------------------------------
 // Fixed-geometry fast path: every span is len bytes at base + i*stride with
 // base, stride and len multiples of 4 and len <= 4 KiB, so a span is K rounds
 // (K = ceil(len/256), a template parameter) with no head/tail bytes and the
@@ -1227,6 +1466,12 @@ __global__ __launch_bounds__(256) void crc32c_scatter_kernel(SpanBatch a, SplitW
 // ---------------------------------------------------------------------------
 // Host-side launchers (called from crc32c_capi.hip through crc32c_device.h).
 // ---------------------------------------------------------------------------
+hipError_t launch_span1(const SpanBatch& a, bool verify, int grid, hipStream_t s) {
+  if (verify) crc32c_span1_kernel<true><<<grid, kThreads, 0, s>>>(a);
+  else crc32c_span1_kernel<false><<<grid, kThreads, 0, s>>>(a);
+  return hipGetLastError();
+}
+
 hipError_t launch_span(const SpanBatch& a, bool verify, int grid, hipStream_t s) {
   // Log records (LOG_HEADER) are short: the variant that skips padding rounds.
   const bool skip = (a.flags & kFlagLogHeader) != 0 && a.role == kRoleSpans;
