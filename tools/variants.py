@@ -36,6 +36,33 @@ VDIR = os.path.join(ROOT, "tools", "vlib")
 MEASURE_ONLY = [("crc32c_capi.hip", "  ctx.status = SelfTest(ctx);\n", "  (void)SelfTest(ctx);\n")]
 
 # name -> [(file under prismdb_amd/csrc, old text, new text), ...]
+LOOP_OLD = '        issue(tk[3], wb[3], eb[3]);\n        constexpr int kYounger = 3 * (kRounds + 1);  // the three younger tasks\n        for (;;) {\n#pragma unroll\n          for (int q = 0; q < 4; ++q) {\n            wait_task<kYounger>(wb[q], eb[q]);\n            if (tk[q].valid()) fold1(tk[q], wb[q], eb[q]);\n            // tasks are made in sequence: the next one invalid, all are\n            if (!tk[(q + 1) & 3].valid()) goto drained1;\n            tk[q] = static_task(jc[0], 0u, tk[(q + 3) & 3]);\n            issue(tk[q], wb[q], eb[q]);\n          }\n        }\n      drained1:\n#pragma unroll\n        for (int q = 0; q < 4; ++q) wait_task<0>(wb[q], eb[q]);\n'
+INIT_OLD = '        tk[2] = static_task(jc[0], 0u, tk[1]);\n        tk[3] = static_task(jc[0], 0u, tk[2]);\n      } else {'
+
+
+def _depth_spec(D):
+    loop_new = (f"        for (int q = {D - 1}; q < {D}; ++q) issue(tk[q], wb[q], eb[q]);\n"
+                f"        constexpr int kYounger = {D - 1} * (kRounds + 1);\n"
+                "        for (;;) {\n#pragma unroll\n"
+                f"          for (int q = 0; q < {D}; ++q) {{\n"
+                "            wait_task<kYounger>(wb[q], eb[q]);\n"
+                "            if (tk[q].valid()) fold1(tk[q], wb[q], eb[q]);\n"
+                f"            if (!tk[(q + 1) % {D}].valid()) goto drained1;\n"
+                f"            tk[q] = static_task(jc[0], 0u, tk[(q + {D - 1}) % {D}]);\n"
+                "            issue(tk[q], wb[q], eb[q]);\n          }\n        }\n      drained1:\n#pragma unroll\n"
+                f"        for (int q = 0; q < {D}; ++q) wait_task<0>(wb[q], eb[q]);\n")
+    init_new = ("        tk[2] = none;\n        tk[3] = none;\n      } else {" if D == 2 else
+                "        tk[2] = static_task(jc[0], 0u, tk[1]);\n        tk[3] = none;\n      } else {")
+    return [("crc32c_direct.hip", "  const bool two = a.n <= 16ull * (uint64_t)grid * kDirectWaves;\n",
+             "  const bool two = a.n == 0;  // (variant: one sequence always)\n"),
+            ("crc32c_direct.hip", "    constexpr int kFirst = kStreams == 1 ? 3 : 2;\n",
+             f"    constexpr int kFirst = kStreams == 1 ? {D - 1} : 2;\n"),
+            ("crc32c_direct.hip", INIT_OLD, init_new),
+            ("crc32c_direct.hip", LOOP_OLD, loop_new)]
+
+
+D2_SPEC = _depth_spec(2)
+D3_SPEC = _depth_spec(3)
 VARIANTS = {
     "base": [],
     # an identical copy under another name: A/A check of the harness
@@ -169,6 +196,15 @@ VARIANTS = {
     # two slots of two streams (positions mod 2): a fold waits for two tasks
     # and runs two LDS chains (tools/patches/crc32c_direct_ring22.hip)
     "ring22": [("crc32c_direct.hip", "@file", "tools/patches/crc32c_direct_ring22.hip")],
+    # one task sequence (no pairs) with a ring of D single-task slots, D = 2
+    # or 3: fewer bytes in flight per wave (a file-sized call requests 25 or
+    # 37 MB at once instead of 50), so each wave's data should come back
+    # earlier and spread out
+    "d2": D2_SPEC,
+    "d3": D3_SPEC,
+    # one sequence always (the 4-slot ring), whatever the batch size
+    "one": [("crc32c_direct.hip", "  const bool two = a.n <= 16ull * (uint64_t)grid * kDirectWaves;\n",
+             "  const bool two = a.n == 0;  // (variant: one sequence always)\n")],
     # one task (17 loads) in flight before the table barrier instead of three:
     # the barrier then waits on fewer queued loads, the other three tasks go
     # out right after it
