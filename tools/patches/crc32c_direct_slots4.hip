@@ -12,14 +12,13 @@
 //   static run   wave w < K owns q or q + 1 consecutive spans (<= 64; lane j
 //                holds span j's descriptor).  Its spans of up to kRingChunks
 //                (32) chunks of 4 KiB -- all the data blocks of an SST -- go
-//                through an inline-asm ring of two single-task slots, one
+//                through an inline-asm ring of four single-task slots, one
 //                task sequence (run positions in order, a span's chunks one
 //                after another, the register carried between them): a wave
-//                waits for its older task and folds it as soon as it lands
-//                (round 4; two slots of three streams before: a file's whole
-//                read went out at once and the folds bunched at its end).
-//                Counted vmcnt waits, one coalesced store of the run's
-//                results.
+//                waits for its oldest task only and folds it as soon as it
+//                lands (round 4; two slots of three streams before, whose
+//                folds bunched at the end of a file-sized call).  Counted
+//                vmcnt waits, one coalesced store of the run's results.
 //   long spans   (more than kRingChunks chunks) are found by their run's wave
 //                first and cut into T tickets of g = 2^lg chunks (T <= 64, or
 //                up to 4096 when the batch has fewer spans than waves; lg in
@@ -190,8 +189,15 @@ constexpr uint32_t kHelpChunks = 256;
 constexpr uint64_t kHelpPoll = 300u;
 static_assert(kDirectMaxSpans < kNullEntry, "span indices fit the entry's 24-bit field");
 
-template <bool kVerify>
+// kStreams: 1 = one task sequence through four single-task slots (a fold
+// waits for the oldest task only); 2 = two sequences (run positions of each
+// parity) through two slots of a task pair (a fold waits for the pair and
+// runs two LDS chains).  The host takes 2 for batches of a few spans per wave
+// (an SST file: a wave's chain of one-chain folds was the tail of the call)
+// and 1 for more (launch_direct).
+template <bool kVerify, int kStreams>
 __global__ __launch_bounds__(kDirectThreads) void crc32c_direct_kernel(SpanBatch a, DirectWs d) {
+  static_assert(kStreams == 1 || kStreams == 2, "one or two task sequences");
   const uint32_t n = (uint32_t)a.n;  // <= kDirectMaxSpans, <= 64 per wave
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = tid & 63u;
@@ -354,16 +360,18 @@ __global__ __launch_bounds__(kDirectThreads) void crc32c_direct_kernel(SpanBatch
     // writes and barrier: those then overlap the first data round trip.
     const uint64_t inrun = m >= 64u ? ~0ull : (1ull << m) - 1ull;
     const uint64_t shortm = inrun & ~lm;
-    // The next task after `prev` (the newest one): the next chunk of prev's
-    // span, or chunk 0 of the next ring span at or after run position j.
-    auto static_task = [&](uint32_t& j, const DTask& prev) -> DTask {
+    // Sequence st's next task after `prev` (its newest one): the next chunk of
+    // prev's span, or chunk 0 of the sequence's next ring span at or after run
+    // position j (every position, or those of parity st).
+    auto static_task = [&](uint32_t& j, uint32_t st, const DTask& prev) -> DTask {
       if (prev.valid() && !prev.rlast()) {
         DTask t = prev;
         t.f += 1u << 22;
         return t;
       }
       const uint64_t from = j >= 64u ? 0ull : ~0ull << j;
-      const uint64_t avail = shortm & from;
+      const uint64_t par = kStreams == 1 ? ~0ull : 0x5555555555555555ull << st;
+      const uint64_t avail = shortm & par & from;
       if (avail == 0u) {
         j = 64u;
         DTask t = geometry(base, 0u);
@@ -378,7 +386,7 @@ __global__ __launch_bounds__(kDirectThreads) void crc32c_direct_kernel(SpanBatch
       t.b = sbase + p;
       t.c = 0;  // (the ring reads the chunk from f)
       t.c1 = 1;
-      j = p + 1u;
+      j = p + (uint32_t)kStreams;
       return t;
     };
     // 17 loads per task, always: 16 body dwords of chunk t.c (the buffer
@@ -423,32 +431,43 @@ __global__ __launch_bounds__(kDirectThreads) void crc32c_direct_kernel(SpanBatch
       if (kVerify && last && lane >= 6u && lane < 10u) eoff = hwin ? lane - 6u : sat((uint64_t)len + (lane - 6u));
       e = buf_ubyte(re, eoff);
     };
-    // The ring: one sequence of tasks (run positions in order, a span's
-    // chunks one after another) through TWO single-task slots: a wave waits
-    // for its older task (the younger one's 17 loads stay in flight) and
-    // folds it as soon as it has landed.  Two tasks in flight per wave are
-    // 25 MB over the chip, enough to keep HBM busy; more only lengthen every
-    // wave's wait for its first data (a file-sized call's whole read used to
-    // go out at once), and the folds then bunch up behind the last arrivals.
-    // (slots 2 and 3 stay unused: declared with two entries, hipcc copied
-    // in-flight ring registers at the loop head, tools/check_inflight.py)
+    // The ring: four slots.  kStreams 1: one sequence of tasks (run positions
+    // in order, a span's chunks one after another), a wave waits for its
+    // OLDEST task only (three younger tasks, 51 loads, stay in flight) and
+    // folds it as soon as it has landed.  kStreams 2: slots (0, 1) and (2, 3)
+    // are task pairs of two sequences (positions of parity 0 and 1), a wave
+    // waits for the older pair (the younger pair's 34 loads stay in flight)
+    // and folds both tasks as two interleaved LDS chains.
     DTask tk[4];
     uint32_t wb[4][kRounds];
     uint32_t eb[4];
-    uint32_t jc = 0u;
+    uint32_t jc[2] = {0u, 1u};
     {
       DTask none = geometry(base, 0u);
       none.f = 0;
-      tk[0] = static_task(jc, none);  // (none without a run)
-      tk[1] = static_task(jc, tk[0]);
+      if constexpr (kStreams == 1) {
+        jc[0] = 0u;
+        tk[0] = static_task(jc[0], 0u, none);  // (none without a run)
+        tk[1] = static_task(jc[0], 0u, tk[0]);
+        tk[2] = static_task(jc[0], 0u, tk[1]);
+        tk[3] = static_task(jc[0], 0u, tk[2]);
+      } else {
+        tk[0] = static_task(jc[0], 0u, none);
+        tk[1] = static_task(jc[1], 1u, none);
+        tk[2] = static_task(jc[0], 0u, tk[0]);
+        tk[3] = static_task(jc[1], 1u, tk[1]);
+      }
     }
     // Every wave runs the ring (a wave without a run: empty tasks, whose
     // range-checked loads touch no memory, and no folds), so the ring's
     // registers have one definition on every path: hipCC then never copies
-    // an in-flight register at a merge (tools/check_inflight.py).  The first
-    // task's loads go out before the table fill's LDS writes and barrier.
-    issue(tk[0], wb[0], eb[0]);
-    tables_wait<kRounds + 1>(tr);  // its 17 loads stay in flight
+    // an in-flight register at a merge (tools/check_inflight.py).
+    // The first tasks' loads go out before the table fill's LDS writes and
+    // barrier (three tasks, or the first pair).
+    constexpr int kFirst = kStreams == 1 ? 3 : 2;
+#pragma unroll
+    for (int q = 0; q < kFirst; ++q) issue(tk[q], wb[q], eb[q]);
+    tables_wait<kFirst * (kRounds + 1)>(tr);  // those loads stay in flight
     tables_store<kDirectThreads>(lds, tr, tid);
     // Group barrier for the LDS image.  Not __syncthreads(): its release
     // fence waits for every outstanding load (vmcnt(0)), slot 0's included.
@@ -673,50 +692,104 @@ __global__ __launch_bounds__(kDirectThreads) void crc32c_direct_kernel(SpanBatch
     };
 
     // ---- the static run: its ring spans in run order (long ones skipped),
-    // two single-task slots (a wait leaves the younger task's 17 loads in
-    // flight), inline-asm loads, counted waits, one LDS chain per fold (the
-    // 12 waves of a CU interleave theirs).  Measured in one process,
-    // alternating order (profiles/r04/r04b_variants_ring4_slot1late_tablesfirst.json,
-    // r04g_variants.json, r04j_variants_ring_depth.json): against round 3's
-    // two slots of three streams, four single-task slots gained 3-10 %
-    // (config-3 spans +10.5 %); against four slots, two gain again: one
-    // sealed SST file 4135 against 3865 GB/s (16.4 us), verified +9.8 %,
-    // two files +10.6 %, three +9.2 %, seven +5.8 %.
+    // four slots (68 loads in flight; a wait leaves at most 51 younger loads
+    // in flight, under vmcnt's 63), inline-asm loads, counted waits.
+    // Measured against round 3's two slots of three streams
+    // (profiles/r04/r04b_variants_ring4_slot1late_tablesfirst.json,
+    // r04f_variants.json; one process, alternating order): one sequence, a
+    // sealed SST file 19.0 against 19.9 us, config-3 spans +10.5 %, random
+    // spans +6.0 %, 4 KiB spans -0.4 %, seven files verified in one call
+    // +11 %; two sequences, one sealed SST file 17.8 us (+8 % over one
+    // sequence) but seven files -4 %.
     {
-      uint32_t carry = 0u;  // the register between the chunks of the current span
+      // a sequence's register between the chunks of its current span
+      uint32_t carry[2] = {0u, 0u};
       // The initial register, fed the head bytes, enters chunk 0 with its
       // body word 0 (a zero injection for a later chunk, which continues the
       // carried register); realigned and reduced every task, and a span's
-      // last chunk finishes it.
-      auto fold = [&](const DTask& t, uint32_t (&w)[kRounds], const uint32_t e) {
+      // last chunk finishes it.  Sequences are folded unconditionally (under
+      // per-sequence branches the head feeds and the realignments of round
+      // 3's three streams ran one after the other).
+      auto fold = [&](const DTask* t, uint32_t (*w)[kRounds], const uint32_t* e) {
+        uint32_t r[kStreams], acc[kStreams];
+#pragma unroll
+        for (int st = 0; st < kStreams; ++st) {
+          const bool c0 = t[st].rc() == 0u;
+          r[st] = feed_short(ss, lane, readlane(vinit, t[st].slot()) ^ kConditioning, edge_head(e[st], t[st].h()),
+                             t[st].h());
+          acc[st] = c0 ? 0u : carry[st];
+          if (t[st].z) inject(w[st], t[st].pad(), c0 ? r[st] : 0u);
+        }
+#pragma unroll
+        for (int j = 0; j < kRounds; ++j) {
+#pragma unroll
+          for (int st = 0; st < kStreams; ++st) acc[st] = step256(lds, tab, acc[st], w[st][j]);
+        }
+        uint32_t v[kStreams];
+#pragma unroll
+        for (int st = 0; st < kStreams; ++st) v[st] = realign(lds, nibtab, acc[st]);
+#pragma unroll
+        for (int st = 0; st < kStreams; ++st) {
+          carry[st] = acc[st];
+          const uint32_t bv = wave_xor(v[st]);
+          if (t[st].valid() && t[st].rlast())
+            finish(t[st], t[st].z ? bv : r[st], edge_tail(e[st], t[st].t()), edge_stored(e[st]), true);
+        }
+      };
+      // one sequence: the fold of one task (the pointer form of the fold
+      // below made hipcc copy in-flight ring registers in this instance)
+      auto fold1 = [&](const DTask& t, uint32_t (&w)[kRounds], const uint32_t e) {
         const bool c0 = t.rc() == 0u;
         const uint32_t r =
             feed_short(ss, lane, readlane(vinit, t.slot()) ^ kConditioning, edge_head(e, t.h()), t.h());
-        uint32_t acc = c0 ? 0u : carry;
+        uint32_t acc = c0 ? 0u : carry[0];
         if (t.z) inject(w, t.pad(), c0 ? r : 0u);
 #pragma unroll
         for (int j = 0; j < kRounds; ++j) acc = step256(lds, tab, acc, w[j]);
         const uint32_t v = realign(lds, nibtab, acc);
-        carry = acc;
+        carry[0] = acc;
         const uint32_t bv = wave_xor(v);
         if (t.valid() && t.rlast()) finish(t, t.z ? bv : r, edge_tail(e, t.t()), edge_stored(e), true);
       };
-      issue(tk[1], wb[1], eb[1]);
-      constexpr int kYounger = kRounds + 1;  // the younger task
-      for (;;) {
+      if constexpr (kStreams == 1) {
+        issue(tk[3], wb[3], eb[3]);
+        constexpr int kYounger = 3 * (kRounds + 1);  // the three younger tasks
+        for (;;) {
 #pragma unroll
-        for (int q = 0; q < 2; ++q) {
-          wait_task<kYounger>(wb[q], eb[q]);
-          if (tk[q].valid()) fold(tk[q], wb[q], eb[q]);
-          // tasks are made in sequence: the next one invalid, all are
-          if (!tk[q ^ 1].valid()) goto drained;
-          tk[q] = static_task(jc, tk[q ^ 1]);
-          issue(tk[q], wb[q], eb[q]);
+          for (int q = 0; q < 4; ++q) {
+            wait_task<kYounger>(wb[q], eb[q]);
+            if (tk[q].valid()) fold1(tk[q], wb[q], eb[q]);
+            // tasks are made in sequence: the next one invalid, all are
+            if (!tk[(q + 1) & 3].valid()) goto drained1;
+            tk[q] = static_task(jc[0], 0u, tk[(q + 3) & 3]);
+            issue(tk[q], wb[q], eb[q]);
+          }
         }
-      }
-    drained:
+      drained1:
 #pragma unroll
-      for (int q = 0; q < 2; ++q) wait_task<0>(wb[q], eb[q]);
+        for (int q = 0; q < 4; ++q) wait_task<0>(wb[q], eb[q]);
+      } else {
+        issue(tk[2], wb[2], eb[2]);
+        issue(tk[3], wb[3], eb[3]);
+        constexpr int kYounger = 2 * (kRounds + 1);  // the younger pair
+        for (;;) {
+#pragma unroll
+          for (int q = 0; q < 4; q += 2) {
+            wait_task<kYounger>(wb[q], eb[q]);
+            wait_task<kYounger>(wb[q + 1], eb[q + 1]);
+            if (tk[q].valid() || tk[q + 1].valid()) fold(&tk[q], &wb[q], &eb[q]);
+            // a sequence's next task invalid, all of its later ones are
+            if (!tk[q ^ 2].valid() && !tk[(q + 1) ^ 2].valid()) goto drained2;
+            tk[q] = static_task(jc[0], 0u, tk[q ^ 2]);
+            tk[q + 1] = static_task(jc[1], 1u, tk[(q + 1) ^ 2]);
+            issue(tk[q], wb[q], eb[q]);
+            issue(tk[q + 1], wb[q + 1], eb[q + 1]);
+          }
+        }
+      drained2:
+#pragma unroll
+        for (int q = 0; q < 4; ++q) wait_task<0>(wb[q], eb[q]);
+      }
     }
 
     // ---- workers
@@ -792,10 +865,18 @@ __global__ __launch_bounds__(kDirectThreads) void crc32c_direct_kernel(SpanBatch
 
 hipError_t launch_direct(const SpanBatch& a, bool verify, int grid, const DirectWs& d, hipStream_t s,
                          hipEvent_t done) {
-  if (verify)
-    hipExtLaunchKernelGGL(crc32c_direct_kernel<true>, dim3(grid), dim3(kDirectThreads), 0, s, nullptr, done, 0u, a, d);
+  // Two task sequences while a wave's static run is short (<= 16 spans: up to
+  // about three SST files), one beyond.
+  const bool two = a.n <= 16ull * (uint64_t)grid * kDirectWaves;
+  const dim3 g(grid), b(kDirectThreads);
+  if (verify && two)
+    hipExtLaunchKernelGGL((crc32c_direct_kernel<true, 2>), g, b, 0, s, nullptr, done, 0u, a, d);
+  else if (verify)
+    hipExtLaunchKernelGGL((crc32c_direct_kernel<true, 1>), g, b, 0, s, nullptr, done, 0u, a, d);
+  else if (two)
+    hipExtLaunchKernelGGL((crc32c_direct_kernel<false, 2>), g, b, 0, s, nullptr, done, 0u, a, d);
   else
-    hipExtLaunchKernelGGL(crc32c_direct_kernel<false>, dim3(grid), dim3(kDirectThreads), 0, s, nullptr, done, 0u, a, d);
+    hipExtLaunchKernelGGL((crc32c_direct_kernel<false, 1>), g, b, 0, s, nullptr, done, 0u, a, d);
   return hipGetLastError();
 }
 

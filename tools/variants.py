@@ -36,33 +36,6 @@ VDIR = os.path.join(ROOT, "tools", "vlib")
 MEASURE_ONLY = [("crc32c_capi.hip", "  ctx.status = SelfTest(ctx);\n", "  (void)SelfTest(ctx);\n")]
 
 # name -> [(file under prismdb_amd/csrc, old text, new text), ...]
-LOOP_OLD = '        issue(tk[3], wb[3], eb[3]);\n        constexpr int kYounger = 3 * (kRounds + 1);  // the three younger tasks\n        for (;;) {\n#pragma unroll\n          for (int q = 0; q < 4; ++q) {\n            wait_task<kYounger>(wb[q], eb[q]);\n            if (tk[q].valid()) fold1(tk[q], wb[q], eb[q]);\n            // tasks are made in sequence: the next one invalid, all are\n            if (!tk[(q + 1) & 3].valid()) goto drained1;\n            tk[q] = static_task(jc[0], 0u, tk[(q + 3) & 3]);\n            issue(tk[q], wb[q], eb[q]);\n          }\n        }\n      drained1:\n#pragma unroll\n        for (int q = 0; q < 4; ++q) wait_task<0>(wb[q], eb[q]);\n'
-INIT_OLD = '        tk[2] = static_task(jc[0], 0u, tk[1]);\n        tk[3] = static_task(jc[0], 0u, tk[2]);\n      } else {'
-
-
-def _depth_spec(D):
-    loop_new = (f"        for (int q = {D - 1}; q < {D}; ++q) issue(tk[q], wb[q], eb[q]);\n"
-                f"        constexpr int kYounger = {D - 1} * (kRounds + 1);\n"
-                "        for (;;) {\n#pragma unroll\n"
-                f"          for (int q = 0; q < {D}; ++q) {{\n"
-                "            wait_task<kYounger>(wb[q], eb[q]);\n"
-                "            if (tk[q].valid()) fold1(tk[q], wb[q], eb[q]);\n"
-                f"            if (!tk[(q + 1) % {D}].valid()) goto drained1;\n"
-                f"            tk[q] = static_task(jc[0], 0u, tk[(q + {D - 1}) % {D}]);\n"
-                "            issue(tk[q], wb[q], eb[q]);\n          }\n        }\n      drained1:\n#pragma unroll\n"
-                f"        for (int q = 0; q < {D}; ++q) wait_task<0>(wb[q], eb[q]);\n")
-    init_new = ("        tk[2] = none;\n        tk[3] = none;\n      } else {" if D == 2 else
-                "        tk[2] = static_task(jc[0], 0u, tk[1]);\n        tk[3] = none;\n      } else {")
-    return [("crc32c_direct.hip", "  const bool two = a.n <= 16ull * (uint64_t)grid * kDirectWaves;\n",
-             "  const bool two = a.n == 0;  // (variant: one sequence always)\n"),
-            ("crc32c_direct.hip", "    constexpr int kFirst = kStreams == 1 ? 3 : 2;\n",
-             f"    constexpr int kFirst = kStreams == 1 ? {D - 1} : 2;\n"),
-            ("crc32c_direct.hip", INIT_OLD, init_new),
-            ("crc32c_direct.hip", LOOP_OLD, loop_new)]
-
-
-D2_SPEC = _depth_spec(2)
-D3_SPEC = _depth_spec(3)
 VARIANTS = {
     "base": [],
     # an identical copy under another name: A/A check of the harness
@@ -165,14 +138,14 @@ VARIANTS = {
          "    asm volatile(\"s_waitcnt lgkmcnt(0)\\n\\ts_barrier\" ::: \"memory\");\n"
          "    ts2 = __builtin_amdgcn_s_memrealtime();\n"),
         ("crc32c_direct.hip",
-         "            if (tk[q].valid()) fold(tk[q], wb[q], eb[q]);\n",
-         "            if (tsw == 0) tsw = __builtin_amdgcn_s_memrealtime();\n"
-         "            if (tk[q].valid()) fold(tk[q], wb[q], eb[q]);\n"
-         "            if (ts3 == 0) ts3 = __builtin_amdgcn_s_memrealtime();\n"),
+         "          if (tk[q].valid()) fold(tk[q], wb[q], eb[q]);\n",
+         "          if (tsw == 0) tsw = __builtin_amdgcn_s_memrealtime();\n"
+         "          if (tk[q].valid()) fold(tk[q], wb[q], eb[q]);\n"
+         "          if (ts3 == 0) ts3 = __builtin_amdgcn_s_memrealtime();\n"),
         ("crc32c_direct.hip",
-         "        for (int q = 0; q < 4; ++q) wait_task<0>(wb[q], eb[q]);\n      }\n",
-         "        for (int q = 0; q < 4; ++q) wait_task<0>(wb[q], eb[q]);\n      }\n"
-         "        ts4 = __builtin_amdgcn_s_memrealtime();\n"),
+         "      for (int q = 0; q < 2; ++q) wait_task<0>(wb[q], eb[q]);\n    }\n",
+         "      for (int q = 0; q < 2; ++q) wait_task<0>(wb[q], eb[q]);\n    }\n"
+         "      ts4 = __builtin_amdgcn_s_memrealtime();\n"),
         ("crc32c_direct.hip", "    }\n  }\n\n}\n\nhipError_t launch_direct",
          "    }\n  }\n  if (a.out != nullptr && lane < 8u) {\n"
          "    const uint64_t ts5 = __builtin_amdgcn_s_memrealtime();\n"
@@ -196,24 +169,9 @@ VARIANTS = {
     # two slots of two streams (positions mod 2): a fold waits for two tasks
     # and runs two LDS chains (tools/patches/crc32c_direct_ring22.hip)
     "ring22": [("crc32c_direct.hip", "@file", "tools/patches/crc32c_direct_ring22.hip")],
-    # one task sequence (no pairs) with a ring of D single-task slots, D = 2
-    # or 3: fewer bytes in flight per wave (a file-sized call requests 25 or
-    # 37 MB at once instead of 50), so each wave's data should come back
-    # earlier and spread out
-    "d2": D2_SPEC,
-    "d3": D3_SPEC,
-    # one sequence always (the 4-slot ring), whatever the batch size
-    "one": [("crc32c_direct.hip", "  const bool two = a.n <= 16ull * (uint64_t)grid * kDirectWaves;\n",
-             "  const bool two = a.n == 0;  // (variant: one sequence always)\n")],
-    # one task (17 loads) in flight before the table barrier instead of three:
-    # the barrier then waits on fewer queued loads, the other three tasks go
-    # out right after it
-    "t1": [("crc32c_direct.hip",
-            "#pragma unroll\n    for (int q = 0; q < 3; ++q) issue(tk[q], wb[q], eb[q]);\n"
-            "    tables_wait<3 * (kRounds + 1)>(tr);  // the three tasks' 51 loads stay in flight\n",
-            "    issue(tk[0], wb[0], eb[0]);\n    tables_wait<kRounds + 1>(tr);\n"),
-           ("crc32c_direct.hip", "        issue(tk[3], wb[3], eb[3]);\n",
-            "#pragma unroll\n        for (int q = 1; q < 4; ++q) issue(tk[q], wb[q], eb[q]);\n")],
+    # the ring before two single-task slots: four slots, and two task
+    # sequences in pairs for short runs (tools/patches/crc32c_direct_slots4.hip)
+    "slots4": [("crc32c_direct.hip", "@file", "tools/patches/crc32c_direct_slots4.hip")],
     # the one-launch kernel at 16 waves per CU (1024-thread groups; needs
     # <= 128 VGPRs): fewer tasks per wave, so a wave's chain of folds ends sooner
     "w16": [("crc32c_device.h", "constexpr int kDirectThreads = 768;", "constexpr int kDirectThreads = 1024;")],
@@ -227,13 +185,6 @@ VARIANTS = {
                     '  asm volatile("global_store_dword %0, %1, off" : : "v"(p), "v"(v) : "memory");\n',
                     "  uint8_t* q = const_cast<uint8_t*>(p);\n  q[0] = (uint8_t)v;\n  q[1] = (uint8_t)(v >> 8);\n"
                     "  q[2] = (uint8_t)(v >> 16);\n  q[3] = (uint8_t)(v >> 24);\n")],
-    # the table fill retired before any data load
-    "t0": [("crc32c_direct.hip",
-            "#pragma unroll\n    for (int q = 0; q < 3; ++q) issue(tk[q], wb[q], eb[q]);\n"
-            "    tables_wait<3 * (kRounds + 1)>(tr);  // the three tasks' 51 loads stay in flight\n",
-            "    tables_wait<0>(tr);\n"),
-           ("crc32c_direct.hip", "        issue(tk[3], wb[3], eb[3]);\n",
-            "#pragma unroll\n        for (int q = 0; q < 4; ++q) issue(tk[q], wb[q], eb[q]);\n")],
 }
 
 # the previous commit's kernels (a git worktree under build/:
@@ -242,8 +193,6 @@ VARIANTS["prev"] = [("@src", os.path.join(ROOT, "build", "wt_head", "prismdb_amd
 # combinations
 VARIANTS["tf_ts"] = VARIANTS["tables_first"] + VARIANTS["direct_ts"]
 VARIANTS["tf_lg0_w2"] = VARIANTS["tables_first"] + VARIANTS["lg0"] + VARIANTS["workers2x"]
-VARIANTS["t1_ts"] = VARIANTS["t1"] + VARIANTS["direct_ts"]
-VARIANTS["t0_ts"] = VARIANTS["t0"] + VARIANTS["direct_ts"]
 
 
 def do_build(names):
@@ -389,6 +338,11 @@ def do_run(args, names):
                                          hout.data_ptr(), None, 0, sp), nh * ((64 << 20) - 5 + 16)),
         "adversarial": (lambda n: libs[n][1](buf.data_ptr(), aoff.data_ptr(), alen.data_ptr(), None, len(al),
                                              out.data_ptr(), None, 0, sp), int(al.sum()) + 16 * len(al)),
+        # the first 2^17 spans of the mixed and the random batch: one launch of the one-launch kernel
+        "mixed17": (lambda n: libs[n][1](buf.data_ptr(), moff.data_ptr(), mlen.data_ptr(), None, 1 << 17,
+                                         out.data_ptr(), None, 0, sp), int(ml[:1 << 17].sum()) + 16 * (1 << 17)),
+        "adv17": (lambda n: libs[n][1](buf.data_ptr(), aoff.data_ptr(), alen.data_ptr(), None, 1 << 17,
+                                       out.data_ptr(), None, 0, sp), int(al[:1 << 17].sum()) + 16 * (1 << 17)),
         "file_fixed": (lambda n: libs[n][0](buf.data_ptr(), 3992, 3988, nfd, 0, fout.data_ptr(), None, 0, sp),
                        nfd * (3988 + 4)),
         "file_desc": (lambda n: libs[n][1](buf.data_ptr(), foff.data_ptr(), flen.data_ptr(), None, nfd + 1,
