@@ -180,6 +180,22 @@ VARIANTS = {
     "noseal": [("crc32c_direct.hip",
                 "        store_le32(reinterpret_cast<const uint8_t*>(hdr ? p - kLogCrcBack : body + gz + ((gf >> 12) & 3u)), res);\n",
                 "        (void)p;\n        (void)body;\n")] + MEASURE_ONLY,
+    # measurement-only (32 bytes around each trailer overwritten): the ring
+    # spans' trailers stored as whole aligned 32-B sectors (two 16-B stores)
+    # instead of one 4-B store -- whether partial-sector writes are the cost
+    "sector32": [("crc32c_direct.hip",
+                  "        store_le32(reinterpret_cast<const uint8_t*>(hdr ? p - kLogCrcBack : body + gz + ((gf >> 12) & 3u)), res);\n",
+                  "        {\n"
+                  "          const uint64_t ta = (hdr ? p - kLogCrcBack : body + gz + ((gf >> 12) & 3u)) & ~31ull;\n"
+                  "          const u32x4 vv = {res, res, res, res};\n"
+                  "          asm volatile(\"global_store_dwordx4 %0, %1, off\\n\\tglobal_store_dwordx4 %0, %1, off offset:16\"\n"
+                  "                       : : \"v\"(ta), \"v\"(vv) : \"memory\");\n"
+                  "        }\n")] + MEASURE_ONLY,
+    # 16 waves per CU with the ticket path folding one chunk per step (its
+    # two-chunk steps held 64 VGPRs): does the kernel then fit 128 VGPRs, and
+    # do shorter runs per wave (~4 spans of a file instead of ~5.5) pay?
+    "w16g1": [("crc32c_device.h", "constexpr int kDirectThreads = 768;", "constexpr int kDirectThreads = 1024;"),
+              ("crc32c_direct.hip", "      constexpr int kG = 2;\n", "      constexpr int kG = 1;\n")],
     # trailers as four byte stores (before round 4: one dword store)
     "bytestores": [("crc32c_fold.h",
                     '  asm volatile("global_store_dword %0, %1, off" : : "v"(p), "v"(v) : "memory");\n',
