@@ -29,7 +29,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-VDIR = os.path.join(ROOT, "tools", "vlib")
+VDIR = os.environ.get("PRISMDB_VLIB", os.path.join(ROOT, "tools", "vlib"))  # (override: trial builds)
 
 # Measurement-only variants compute wrong results on purpose: their device
 # self-test would refuse the device, so it is reported but not enforced.
@@ -196,6 +196,58 @@ VARIANTS = {
     # do shorter runs per wave (~4 spans of a file instead of ~5.5) pay?
     "w16g1": [("crc32c_device.h", "constexpr int kDirectThreads = 768;", "constexpr int kDirectThreads = 1024;"),
               ("crc32c_direct.hip", "      constexpr int kG = 2;\n", "      constexpr int kG = 1;\n")],
+    # WAL seal, measurement only (ignores neighbouring records' crc words in
+    # the same sector): the lane kernel rewrites the whole aligned 32-B
+    # sector holding a record's crc (loaded with the record's last task)
+    # instead of one unaligned dword.  Does seal then reach verify?
+    "walsec": [
+        ("crc32c_kernels.hip",
+         "__device__ __forceinline__ void wait_lane(u32x4 (&w)[8], uint32_t& hd, uint32_t& ed, uint32_t& sc, uint64_t& noff,\n"
+         "                                          uint32_t& nlen, uint32_t& ninit) {\n"
+         "  asm volatile(\"s_waitcnt vmcnt(8)\"\n"
+         "               : \"+v\"(w[0]), \"+v\"(w[1]), \"+v\"(w[2]), \"+v\"(w[3]), \"+v\"(w[4]), \"+v\"(w[5]), \"+v\"(w[6]),\n"
+         "                 \"+v\"(w[7]), \"+v\"(hd), \"+v\"(ed), \"+v\"(sc), \"+v\"(noff), \"+v\"(nlen), \"+v\"(ninit)\n",
+         "__device__ __forceinline__ void wait_lane(u32x4 (&w)[8], uint32_t& hd, uint32_t& ed, uint32_t& sc, uint64_t& noff,\n"
+         "                                          uint32_t& nlen, uint32_t& ninit, u32x4& sa, u32x4& sb) {\n"
+         "  asm volatile(\"s_waitcnt vmcnt(8)\"\n"
+         "               : \"+v\"(w[0]), \"+v\"(w[1]), \"+v\"(w[2]), \"+v\"(w[3]), \"+v\"(w[4]), \"+v\"(w[5]), \"+v\"(w[6]),\n"
+         "                 \"+v\"(w[7]), \"+v\"(hd), \"+v\"(ed), \"+v\"(sc), \"+v\"(noff), \"+v\"(nlen), \"+v\"(ninit), \"+v\"(sa), \"+v\"(sb)\n"),
+        ("crc32c_kernels.hip", "  uint64_t VP[2];\n  auto issue",
+         "  uint64_t VP[2];\n  u32x4 SA[2] = {}, SB[2] = {};\n  auto issue"),
+        ("crc32c_kernels.hip",
+         "      if (kVerify) SC[sl] = asm_load_u32(owned && lastk ? (hdr ? vp - kLogCrcBack : vp + vlen) : zero);\n    }\n",
+         "      if (kVerify) SC[sl] = asm_load_u32(owned && lastk ? (hdr ? vp - kLogCrcBack : vp + vlen) : zero);\n"
+         "      if (!kVerify) {\n"
+         "        const uint64_t sa = owned && lastk ? ((hdr ? vp - kLogCrcBack : vp + vlen) & ~31ull) : zero;\n"
+         "        asm volatile(\"global_load_dwordx4 %0, %1, off\" : \"=v\"(SA[sl]) : \"v\"(sa));\n"
+         "        asm volatile(\"global_load_dwordx4 %0, %1, off offset:16\" : \"=v\"(SB[sl]) : \"v\"(sa));\n"
+         "      }\n    }\n"),
+        ("crc32c_kernels.hip",
+         "          asm volatile(\"global_store_dword %0, %1, off\" : : \"v\"(ta), \"v\"(v) : \"memory\");\n",
+         "          const uint32_t b = (uint32_t)ta & 31u;\n"
+         "          if (b > 28u) {\n"
+         "            asm volatile(\"global_store_dword %0, %1, off\" : : \"v\"(ta), \"v\"(v) : \"memory\");\n"
+         "          } else {\n"
+         "            const uint32_t sh = 8u * (b & 3u), q = b >> 2;\n"
+         "            const uint64_t v64 = (uint64_t)v << sh, m64 = 0xFFFFFFFFull << sh;\n"
+         "            u32x4 s0 = SA[sl], s1 = SB[sl];\n"
+         "            auto put = [&](uint32_t w, uint32_t d) -> uint32_t {\n"
+         "              w = d == q ? (w & ~(uint32_t)m64) | (uint32_t)v64 : w;\n"
+         "              return d == q + 1u ? (w & ~(uint32_t)(m64 >> 32)) | (uint32_t)(v64 >> 32) : w;\n"
+         "            };\n"
+         "            s0[0] = put(s0[0], 0); s0[1] = put(s0[1], 1); s0[2] = put(s0[2], 2); s0[3] = put(s0[3], 3);\n"
+         "            s1[0] = put(s1[0], 4); s1[1] = put(s1[1], 5); s1[2] = put(s1[2], 6); s1[3] = put(s1[3], 7);\n"
+         "            const uint64_t sa = ta & ~31ull;\n"
+         "            asm volatile(\"global_store_dwordx4 %0, %1, off\" : : \"v\"(sa), \"v\"(s0) : \"memory\");\n"
+         "            asm volatile(\"global_store_dwordx4 %0, %1, off offset:16\" : : \"v\"(sa), \"v\"(s1) : \"memory\");\n"
+         "          }\n"),
+        ("crc32c_kernels.hip", '"+v"(HD[0]), "+v"(ED[0]), "+v"(SC[0]) : : "memory");',
+         '"+v"(HD[0]), "+v"(ED[0]), "+v"(SC[0]), "+v"(SA[0]), "+v"(SB[0]) : : "memory");'),
+        ("crc32c_kernels.hip", "      wait_lane(W[sl], HD[sl], ED[sl], SC[sl], noff, nlen, ninit);\n",
+         "      wait_lane(W[sl], HD[sl], ED[sl], SC[sl], noff, nlen, ninit, SA[sl], SB[sl]);\n"),
+        ("crc32c_kernels.hip", '    asm volatile("" : "+v"(HD[sl]), "+v"(ED[sl]), "+v"(SC[sl]));\n',
+         '    asm volatile("" : "+v"(HD[sl]), "+v"(ED[sl]), "+v"(SC[sl]), "+v"(SA[sl]), "+v"(SB[sl]));\n'),
+    ],
     # trailers as four byte stores (before round 4: one dword store)
     "bytestores": [("crc32c_fold.h",
                     '  asm volatile("global_store_dword %0, %1, off" : : "v"(p), "v"(v) : "memory");\n',
@@ -206,6 +258,27 @@ VARIANTS = {
 # the previous commit's kernels (a git worktree under build/:
 # `git worktree add --detach build/wt_head HEAD`)
 VARIANTS["prev"] = [("@src", os.path.join(ROOT, "build", "wt_head", "prismdb_amd", "csrc"), None)]
+# walsafe: walsec + the neighbour check (flag bit 26 of the lane's meta)
+VARIANTS["walsafe"] = [
+    (f, o, n.replace("const uint64_t sa = owned && lastk ?", "const uint64_t sa = owned && lastk && ((vmeta >> 26) & 1u) ?")
+            .replace("          if (b > 28u) {\n", "          if (!((meta >> 26) & 1u)) {\n"))
+    for f, o, n in VARIANTS["walsec"]] + [
+    ("crc32c_kernels.hip",
+     "      vmeta = n4 | (q0 << 16) | (h << 21) | (tb << 23) | ((owned ? 1u : 0u) << 25);\n",
+     "      vmeta = n4 | (q0 << 16) | (h << 21) | (tb << 23) | ((owned ? 1u : 0u) << 25);\n"
+     "      {\n"
+     "        const int src = (int)(((lane + 63u) & 63u) << 2);\n"
+     "        const uint32_t plo = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)noff);\n"
+     "        const uint32_t phi = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)(noff >> 32));\n"
+     "        const uint32_t plen = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)nlen);\n"
+     "        const uint64_t pvp = base + ((uint64_t)phi << 32 | plo);\n"
+     "        const uint64_t ta = vp - kLogCrcBack, sa = ta & ~31ull;\n"
+     "        const uint32_t b = (uint32_t)ta & 31u;\n"
+     "        const bool sec = hdr && owned && b <= 28u && sa + 32u <= vp + vlen &&\n"
+     "                         (b == 0u || (lane != 0u && pvp <= sa && pvp + plen >= ta));\n"
+     "        vmeta |= (sec ? 1u : 0u) << 26;\n"
+     "      }\n"),
+]
 # combinations
 VARIANTS["tf_ts"] = VARIANTS["tables_first"] + VARIANTS["direct_ts"]
 VARIANTS["tf_lg0_w2"] = VARIANTS["tables_first"] + VARIANTS["lg0"] + VARIANTS["workers2x"]
