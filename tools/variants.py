@@ -191,6 +191,29 @@ VARIANTS = {
                   "          asm volatile(\"global_store_dwordx4 %0, %1, off\\n\\tglobal_store_dwordx4 %0, %1, off offset:16\"\n"
                   "                       : : \"v\"(ta), \"v\"(vv) : \"memory\");\n"
                   "        }\n")] + MEASURE_ONLY,
+    # measurement-only, as sector32 but the whole aligned 64-B / 128-B line
+    # around each trailer: does a full-line write spare the memory side a
+    # fill of the line it merges a partial write into?
+    "line64": [("crc32c_direct.hip",
+                "        store_le32(reinterpret_cast<const uint8_t*>(hdr ? p - kLogCrcBack : body + gz + ((gf >> 12) & 3u)), res);\n",
+                "        {\n"
+                "          const uint64_t ta = (hdr ? p - kLogCrcBack : body + gz + ((gf >> 12) & 3u)) & ~63ull;\n"
+                "          const u32x4 vv = {res, res, res, res};\n"
+                "          asm volatile(\"global_store_dwordx4 %0, %1, off\\n\\tglobal_store_dwordx4 %0, %1, off offset:16\\n\\t\"\n"
+                "                       \"global_store_dwordx4 %0, %1, off offset:32\\n\\tglobal_store_dwordx4 %0, %1, off offset:48\"\n"
+                "                       : : \"v\"(ta), \"v\"(vv) : \"memory\");\n"
+                "        }\n")] + MEASURE_ONLY,
+    "line128": [("crc32c_direct.hip",
+                 "        store_le32(reinterpret_cast<const uint8_t*>(hdr ? p - kLogCrcBack : body + gz + ((gf >> 12) & 3u)), res);\n",
+                 "        {\n"
+                 "          const uint64_t ta = (hdr ? p - kLogCrcBack : body + gz + ((gf >> 12) & 3u)) & ~127ull;\n"
+                 "          const u32x4 vv = {res, res, res, res};\n"
+                 "          asm volatile(\"global_store_dwordx4 %0, %1, off\\n\\tglobal_store_dwordx4 %0, %1, off offset:16\\n\\t\"\n"
+                 "                       \"global_store_dwordx4 %0, %1, off offset:32\\n\\tglobal_store_dwordx4 %0, %1, off offset:48\\n\\t\"\n"
+                 "                       \"global_store_dwordx4 %0, %1, off offset:64\\n\\tglobal_store_dwordx4 %0, %1, off offset:80\\n\\t\"\n"
+                 "                       \"global_store_dwordx4 %0, %1, off offset:96\\n\\tglobal_store_dwordx4 %0, %1, off offset:112\"\n"
+                 "                       : : \"v\"(ta), \"v\"(vv) : \"memory\");\n"
+                 "        }\n")] + MEASURE_ONLY,
     # 16 waves per CU with the ticket path folding one chunk per step (its
     # two-chunk steps held 64 VGPRs): does the kernel then fit 128 VGPRs, and
     # do shorter runs per wave (~4 spans of a file instead of ~5.5) pay?
