@@ -214,6 +214,15 @@ VARIANTS = {
                  "                       \"global_store_dwordx4 %0, %1, off offset:96\\n\\tglobal_store_dwordx4 %0, %1, off offset:112\"\n"
                  "                       : : \"v\"(ta), \"v\"(vv) : \"memory\");\n"
                  "        }\n")] + MEASURE_ONLY,
+    # trailer stores with other cache policies: sc1 / sc0 sc1 write through
+    # and drop the line from the XCD's L2, nt streams it -- so the dirty
+    # sectors leave during the kernel instead of at its end-of-kernel write-back?
+    "st_sc1": [("crc32c_fold.h", '  asm volatile("global_store_dword %0, %1, off" : : "v"(p), "v"(v) : "memory");\n',
+                '  asm volatile("global_store_dword %0, %1, off sc1" : : "v"(p), "v"(v) : "memory");\n')],
+    "st_sc0sc1": [("crc32c_fold.h", '  asm volatile("global_store_dword %0, %1, off" : : "v"(p), "v"(v) : "memory");\n',
+                '  asm volatile("global_store_dword %0, %1, off sc0 sc1" : : "v"(p), "v"(v) : "memory");\n')],
+    "st_nt": [("crc32c_fold.h", '  asm volatile("global_store_dword %0, %1, off" : : "v"(p), "v"(v) : "memory");\n',
+                '  asm volatile("global_store_dword %0, %1, off nt" : : "v"(p), "v"(v) : "memory");\n')],
     # 16 waves per CU with the ticket path folding one chunk per step (its
     # two-chunk steps held 64 VGPRs): does the kernel then fit 128 VGPRs, and
     # do shorter runs per wave (~4 spans of a file instead of ~5.5) pay?
