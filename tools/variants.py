@@ -223,6 +223,18 @@ VARIANTS = {
                 '  asm volatile("global_store_dword %0, %1, off sc0 sc1" : : "v"(p), "v"(v) : "memory");\n')],
     "st_nt": [("crc32c_fold.h", '  asm volatile("global_store_dword %0, %1, off" : : "v"(p), "v"(v) : "memory");\n',
                 '  asm volatile("global_store_dword %0, %1, off nt" : : "v"(p), "v"(v) : "memory");\n')],
+    # the lane kernel's 128-B line loads non-temporal (round 2 measured nt
+    # halving the v2 kernel, whose tasks straddled lines; v3's are line-aligned)
+    "lane_nt": [("crc32c_kernels.hip",
+                 '    asm volatile("global_load_dwordx4 %0, %1, off offset:%2" : "=v"(w[J]) : "v"(addr), "n"(16 * J));\n',
+                 '    asm volatile("global_load_dwordx4 %0, %1, off offset:%2 nt" : "=v"(w[J]) : "v"(addr), "n"(16 * J));\n')],
+    # the trailer store before round 4's r04o (plain, no nt) -- against the product's nt
+    "st_plain": [("crc32c_fold.h", '  asm volatile("global_store_dword %0, %1, off nt" : : "v"(p), "v"(v) : "memory");\n',
+                  '  asm volatile("global_store_dword %0, %1, off" : : "v"(p), "v"(v) : "memory");\n')],
+    # the lane kernel's log-header crc stores non-temporal too
+    "lanest_nt": [("crc32c_kernels.hip",
+                   '          asm volatile("global_store_dword %0, %1, off" : : "v"(ta), "v"(v) : "memory");\n',
+                   '          asm volatile("global_store_dword %0, %1, off nt" : : "v"(ta), "v"(v) : "memory");\n')],
     # 16 waves per CU with the ticket path folding one chunk per step (its
     # two-chunk steps held 64 VGPRs): does the kernel then fit 128 VGPRs, and
     # do shorter runs per wave (~4 spans of a file instead of ~5.5) pay?
