@@ -35,6 +35,7 @@
 //   crc32c_span_kernel<verify, log>  everything else, driven by the span
 //                           records; the log-record variant skips chunk 0's
 //                           padding rounds
+//   crc32c_pair_kernel<verify>  large batches of one-task records (pair runs)
 //   crc32c_combine_kernel   stitches segments back into long spans
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -69,7 +70,7 @@ namespace dev {
 // and lets invalid or skipped tasks run through the same code.  Records come
 // through the scalar cache, one span ahead per stream.
 // ---------------------------------------------------------------------------
-template <bool kVerify, bool kSkip, bool kPairs>
+template <bool kVerify, bool kSkip>
 __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
   // Chunk geometry: 4 KiB chunks of 16 rounds; kRoundsLog for the log-record
   // kernel (crc32c_device.h).
@@ -115,43 +116,18 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
   const uint32_t S = 2 * nwaves;
   bool sliced = a.slice_start != nullptr;
   uint32_t K = sliced ? (uint32_t)const_load(a.nslices_dev, 0) : 0u;  // <= n/2 + 32 S + 2; 0: runs
-  // Pair runs: the scan found every record one task (nslices = 0), so the
-  // wave's two streams advance one record per fold together.  Then they share
-  // the wave's runs and take alternate records (stream st: lo + st, lo + st +
-  // 2, ...), so a fold reads two adjacent spans, as the fixed kernel's pairs
-  // do: streams a run apart (128 KiB) cost the fixed kernel 3.7 %
-  // (profiles/r02af_variants_fixed_far_pair.json).  Runs are counted in
-  // pairs of records (pq or pq+1 pairs, <= 32, exactly m per wave), so only
-  // the batch's last run can be odd, and a run is stored once, when stream
-  // 0's last record of it is folded (stream 1's last is in the same fold, or
-  // the fold before in an odd last run).
-  // The host launches the pair-run kernel (kPairs) next to the general one
-  // for large batches (a.pair_kernel); each leaves if the scan's result is
-  // the other's.  As one kernel with a runtime switch, the two paths' scalar
-  // state spilled SGPRs to scratch.
-  constexpr bool pairs = kPairs;
+  // Pair runs: when the scan finds every record one task (nslices = 0) and
+  // the host launched crc32c_pair_kernel next to this one (a.pair_kernel,
+  // large batches), that kernel takes the batch and this one leaves.
   // (not after a segment-workspace overflow: long spans are then folded here
   // as chains of chunks, but the scan counted them one task each)
   const bool pair_batch = sliced && K == 0 && skip_long;
-  if (kPairs ? !pair_batch : (pair_batch && a.pair_kernel != 0u)) return;
+  if (pair_batch && a.pair_kernel != 0u) return;
   // Runs: K = m S runs of q or q+1 records (q <= 63, runs 0..r-1 the longer),
   // exactly m per stream; m >= kRunsPerStream while runs keep >= 1
   // record.  (Runs of 2^lg records left a stream the ceil or floor of K/S.)
   uint32_t rq = 0, rr = 0;
-  if (pairs) {
-    sliced = false;
-    const uint32_t np = (n + 1u) / 2u;  // pairs of records
-    const uint32_t rps = kRunsPerStream;
-    uint32_t m = (uint32_t)(((uint64_t)np + 31ull * nwaves - 1u) / (31ull * nwaves));  // <= 32 pairs a run
-    if (m < rps) {
-      const uint32_t mr = np / nwaves;
-      m = mr < rps ? (mr > m ? mr : m) : rps;
-    }
-    if (m < 1u) m = 1u;
-    K = (uint64_t)m * nwaves < np ? m * nwaves : np;
-    rq = np / K;
-    rr = np % K;
-  } else if (K == 0) {
+  if (K == 0) {
     sliced = false;
     const uint32_t rps = kRunsPerStream;
     uint32_t m = (uint32_t)(((uint64_t)n + 63ull * S - 1u) / (63ull * S));
@@ -167,12 +143,12 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
   // A group whose streams (2 per wave) are all >= K has no slice or run: it
   // leaves before loading the tables (the segment pass of a batch with a few
   // long spans launches the whole grid for a handful of streams).
-  if (blockIdx.x * (pairs ? 1u : 2u) * kWavesPerGroup >= K) return;
+  if (blockIdx.x * 2u * kWavesPerGroup >= K) return;
 
 
   __shared__ uint32_t lds[kLdsWords];
-  const uint32_t kstep = pairs ? nwaves : S;  // a stream's next run: k + kstep
-  constexpr uint32_t bstep = pairs ? 2u : 1u;  // its next record in a run: b + bstep
+  const uint32_t kstep = S;        // a stream's next slice or run: k + kstep
+  constexpr uint32_t bstep = 1u;  // its next record in a run: b + bstep
   load_tables(lds, a.tabs, tid);
   __syncthreads();
   const StrideLanes tab = stride_lanes(lane);
@@ -193,13 +169,9 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
       } else {
         lo = k * rq + (k < rr ? k : rr);
         hi = lo + rq + (k < rr ? 1u : 0u);
-        if (pairs) {  // runs of pairs: records [2 lo, 2 hi)
-          lo *= 2u;
-          hi *= 2u;
-        }
       }
       hi = hi < n ? hi : n;
-      const uint32_t b = lo + (pairs ? st : 0u);
+      const uint32_t b = lo;
       if (b < hi) {
         c.b = b;
         c.lo = lo;
@@ -347,19 +319,6 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
       if (kVerify && a.mismatch != nullptr) __builtin_nontemporal_store((uint8_t)bad[s], a.mismatch + base + lane);
     }
   };
-  // Pair runs: the run ending with stream 0's task t, lanes [0, t.slot() + 1]
-  // (those below n), even lanes from stream 0, odd lanes from stream 1.
-  auto flush_pair = [&](const Task& t) {
-    const uint32_t base = t.b - t.slot();
-    if (lane <= t.slot() + 1u && base + lane < n) {
-      // by masks, not `odd ? res[1] : res[0]`: hipcc folds that select into
-      // res[odd], an indexed array, and moves res and bad to scratch
-      const uint32_t odd = 0u - (lane & 1u);
-      if (a.out != nullptr) __builtin_nontemporal_store(res[0] ^ ((res[0] ^ res[1]) & odd), a.out + base + lane);
-      if (kVerify && a.mismatch != nullptr)
-        __builtin_nontemporal_store((uint8_t)(bad[0] ^ ((bad[0] ^ bad[1]) & odd)), a.mismatch + base + lane);
-    }
-  };
   // End of a span: tail bytes, conditioning, outputs.
   auto finish = [&](int s, const Task& t, uint32_t e, uint32_t body) {
     const uint32_t tl = t.t();
@@ -374,7 +333,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
     }
     if ((a.flags & kFlagWriteTrailer) && lane == 0)
       store_le32(hdr ? t.start() - kLogCrcBack : t.body() + t.r.z + tl, v);
-    if (!pairs && t.last()) flush(s, t);
+    if (t.last()) flush(s, t);
   };
   // Fold the pair (stream 0 task tx in wx, stream 1 task ty in wy).
   auto fold = [&](const Task& tx, uint32_t (&wx)[kR], uint32_t ex, const Task& ty,
@@ -427,15 +386,10 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
     } else if (endy) {
       finish(1, ty, ey, wave_xor(realign(lds, nibtab, ay)));
     }
-    if (pairs) {
-      // the run is complete once stream 0's last record of it is folded
-      if (tx.valid() && tx.last()) flush_pair(tx);
-    } else {
-      // A skipped long span's result comes from the combine pass, but it may
-      // close its slice: the slice's other results are stored now.
-      if (tx.skip() && tx.valid() && tx.last()) flush(0, tx);
-      if (ty.skip() && ty.valid() && ty.last()) flush(1, ty);
-    }
+    // A skipped long span's result comes from the combine pass, but it may
+    // close its slice: the slice's other results are stored now.
+    if (tx.skip() && tx.valid() && tx.last()) flush(0, tx);
+    if (ty.skip() && ty.valid() && ty.last()) flush(1, ty);
   };
 
   // Ring: two slots x two streams, compile-time slot indices (loop unrolled
@@ -447,7 +401,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
   uint32_t eb[2][2];
 #pragma unroll
   for (int st = 0; st < 2; ++st) {
-    open(cur[st], pairs ? wave : 2 * wave + st, (uint32_t)st);
+    open(cur[st], 2 * wave + st, (uint32_t)st);
     tk[0][st] = make_task(cur[st], read_rec(cur[st].b));
     advance(cur[st], (uint32_t)st);
     pend[st] = read_rec(cur[st].b);
@@ -479,6 +433,230 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
 drained:
   // Retire the abandoned slot's loads while their registers are live (see the
   // fixed kernel's drain).  Every slice was stored when its last record retired.
+#pragma unroll
+  for (int sl = 0; sl < 2; ++sl) {
+    wait_task<0>(wb[sl][0], eb[sl][0]);
+    wait_task<0>(wb[sl][1], eb[sl][1]);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Pair runs, lean (crc32c_pair_kernel): the batches the slice scan finds all
+// one-task records (every span one 4 KiB chunk or a skipped long span: SST
+// data blocks, 4 KiB descriptors).  The same schedule as the span kernel's
+// pair runs (K = m * nwaves runs of rq or rq + 1 record pairs, run k of wave
+// k mod nwaves, the two spans of a pair adjacent), folded the way the fixed
+// kernel folds: a ring of two pairs, one in flight while the other folds, and
+// per pair only the run arithmetic, two scalar record reads (one pair ahead)
+// and the two spans' buffer descriptors on the scalar unit.  The span
+// kernel's general cursor (slices, chunk chains, record refills) cost this
+// shape 134 SALU, 20 branches and 171 VALU per span against the fixed
+// kernel's 29 / 1 / 128, and 1046 wave-cycles per span against 822 (PMC,
+// profiles/r04/r04q_*): the general kernel ran SST descriptors at 70 % of
+// the roofline where the fixed kernel runs the same blocks at 80 %.
+// ---------------------------------------------------------------------------
+// One span of a pair step (wave-uniform): body address, body bytes, the
+// register after the head bytes, and f = pad | t << 10 | valid << 12 | skip << 13
+// | slot << 16 (the span's position in its run).
+struct PTask {
+  uint64_t body;
+  uint32_t z, w, f;
+  __device__ uint32_t pad() const { return f & 1023u; }
+  __device__ uint32_t t() const { return (f >> 10) & 3u; }
+  __device__ bool valid() const { return (f >> 12) & 1u; }
+  __device__ bool live() const { return ((f >> 12) & 3u) == 1u; }  // valid, not skipped
+  __device__ uint32_t slot() const { return (f >> 16) & 63u; }
+};
+
+template <bool kVerify>
+__global__ __launch_bounds__(kThreads) void crc32c_pair_kernel(SpanBatch a) {
+  const uint32_t n = (uint32_t)a.n;  // (span role, no list: n_dev is null)
+  // The scan's verdict: pair runs only for an all-one-task batch with the long
+  // spans skipped (the general kernel takes the rest and leaves these).
+  if (a.slice_start == nullptr || (a.overflow != nullptr && *a.overflow != 0u)) return;
+  if ((uint32_t)const_load(a.nslices_dev, 0) != 0u || n == 0u) return;
+  const uint32_t nwaves = gridDim.x * kWavesPerGroup;
+  const uint32_t np = (n + 1u) / 2u;  // record pairs
+  uint32_t m = (uint32_t)(((uint64_t)np + 31ull * nwaves - 1u) / (31ull * nwaves));  // <= 32 pairs a run
+  if (m < kRunsPerStream) {
+    const uint32_t mr = np / nwaves;
+    m = mr < kRunsPerStream ? (mr > m ? mr : m) : kRunsPerStream;
+  }
+  if (m < 1u) m = 1u;
+  const uint32_t K = (uint64_t)m * nwaves < np ? m * nwaves : np;
+  const uint32_t rq = np / K, rr = np % K;
+  if (blockIdx.x * kWavesPerGroup >= K) return;
+
+  __shared__ uint32_t lds[kLdsWords];
+  const uint32_t tid = threadIdx.x;
+  load_tables(lds, a.tabs, tid);
+  __syncthreads();
+  const uint32_t lane = tid & 63u;
+  const uint32_t wave = rfl(blockIdx.x * kWavesPerGroup + (tid >> 6));
+  const StrideLanes tab = stride_lanes(lane);
+  const uint32_t nibtab = 4u * (kTabWords + lane);
+  const ShortShift ss = short_shift_cols(lane);
+  const bool masked = (a.flags & kFlagMask) != 0;
+  const bool seal = (a.flags & kFlagWriteTrailer) != 0;
+
+  // Issue-side cursor: run k = [lo, hi) records, pair i of it.
+  uint32_t k = wave, lo = 0, hi = 0, i = 0;
+  auto run_bounds = [&](uint32_t kk) {
+    lo = 2u * (kk * rq + (kk < rr ? kk : rr));
+    hi = lo + 2u * (rq + (kk < rr ? 1u : 0u));
+    hi = hi < n ? hi : n;
+  };
+  if (k < K) run_bounds(k);
+  // b: the pair's first record (n: none left)
+  auto pair_first = [&]() -> uint32_t { return k < K ? lo + 2u * i : n; };
+  auto step = [&]() {
+    if (k >= K) return;
+    if (lo + 2u * (i + 1u) < hi) {
+      ++i;
+    } else {
+      k += nwaves;
+      i = 0;
+      if (k < K) run_bounds(k);
+    }
+  };
+  auto read_rec = [&](uint32_t b) -> SpanRec {
+    SpanRec r{0u, 0u, 0u, 0u};
+    if (b < n) r = const_load(a.rec, b);
+    return r;
+  };
+  auto make = [&](uint32_t b, const SpanRec& r, uint32_t first) -> PTask {
+    PTask t;
+    const bool valid = b < n && b < hi;
+    t.body = ((uint64_t)(r.y & 0xffffu) << 32) | r.x;
+    t.z = valid ? r.z : 0u;
+    t.w = r.w;
+    const uint32_t skip = valid && ((r.y >> 30) & 1u) ? 1u : 0u;
+    t.f = ((r.y >> 16) & 1023u) | (((r.y >> 28) & 3u) << 10) | ((valid ? 1u : 0u) << 12) | (skip << 13) |
+          ((b - first) << 16);
+    return t;
+  };
+  // 17 loads per span, always: 16 body dwords (chunk 0 right-aligned: the
+  // pad leading words read 0 through the range check) and one edge byte per
+  // lane -- tail bytes (lanes 3-5) and the stored crc (6-9).
+  auto issue = [&](const PTask& t, uint32_t (&w)[kRounds], uint32_t& e) {
+    const bool live = t.live();
+    const uint32_t pad = t.pad(), tl = t.t();
+    u32x4 rb = buffer_rsrc(reinterpret_cast<const uint8_t*>(t.body), live ? t.z : 0u);
+    u32x4 re = buffer_rsrc(reinterpret_cast<const uint8_t*>(t.body + t.z), live ? tl + (kVerify ? 4u : 0u) : 0u);
+    asm volatile("" : "+s"(rb), "+s"(re));  // (scalar-built: tools/check_asm_hazards.py)
+    const int32_t i0 = (int32_t)lane - (int32_t)pad;
+    if (pad == 0) {
+      load_rounds(w, rb, (uint32_t)i0 * 4u);
+    } else if (pad <= 64u) {
+      w[0] = buf_dword<0>(rb, (uint32_t)i0 * 4u);
+      load_rounds_from1(w, rb, (uint32_t)(i0 + 64) * 4u);
+    } else {
+#pragma unroll
+      for (int j = 0; j < kRounds; ++j) w[j] = buf_dword<0>(rb, (uint32_t)(i0 + 64 * j) * 4u);
+    }
+    uint32_t eoff = 0xFFFFFFFFu;
+    if (lane >= 3u && lane < 3u + tl) eoff = lane - 3u;
+    if (kVerify && lane >= 6u && lane < 10u) eoff = tl + (lane - 6u);
+    e = buf_ubyte(re, eoff);
+  };
+
+  uint32_t res = 0u, bad = 0u;
+  auto finish = [&](const PTask& t, uint32_t e, uint32_t body) {
+    const uint32_t tl = t.t();
+    const uint32_t d = tl ? readlane(e, 3) | (readlane(e, 4) << 8) | (readlane(e, 5) << 16) : 0u;
+    const uint32_t crc = feed_short(ss, lane, t.z ? body : t.w, d, tl) ^ kConditioning;
+    const uint32_t v = masked ? mask_crc(crc) : crc;
+    const uint32_t slot = t.slot();
+    res = lane == slot ? v : res;
+    if (kVerify) {
+      const uint32_t stored = readlane(e, 6) | (readlane(e, 7) << 8) | (readlane(e, 8) << 16) | (readlane(e, 9) << 24);
+      bad = lane == slot ? (crc != unmask_crc(stored) ? 1u : 0u) : bad;
+    }
+    if (seal && lane == 0) store_le32(reinterpret_cast<const uint8_t*>(t.body + t.z + tl), v);
+  };
+  // The register enters with body word 0: lane pad % 64 of round pad / 64.
+  auto inject = [&](const PTask& t, uint32_t (&w)[kRounds]) {
+    const uint32_t pad = t.pad(), J = pad >> 6;
+    const uint32_t inj = lane == (pad & 63u) ? t.w : 0u;
+    if (J == 0) {
+      w[0] ^= inj;
+    } else {
+#pragma unroll
+      for (int j = 1; j < kRounds; ++j) w[j] = __builtin_amdgcn_bitop3_b32(w[j], inj, (uint32_t)j == J ? ~0u : 0u, 0x78);
+    }
+  };
+  // Fold a pair; the run's results go out with its last pair (lanes below its
+  // record count: skipped long spans' lanes too, which the combine pass then
+  // overwrites).
+  auto fold = [&](const PTask& tx, uint32_t (&wx)[kRounds], uint32_t ex, const PTask& ty, uint32_t (&wy)[kRounds],
+                  uint32_t ey, uint32_t first, uint32_t cnt, bool last) {
+    const bool lx = tx.live() && tx.z != 0u, ly = ty.live() && ty.z != 0u;
+    if (lx) inject(tx, wx);
+    if (ly) inject(ty, wy);
+    uint32_t ax = wx[0], ay = wy[0];
+#pragma unroll
+    for (int j = 1; j < kRounds; ++j) {
+      ax = step256(lds, tab, ax, wx[j]);
+      ay = step256(lds, tab, ay, wy[j]);
+    }
+    const uint32_t bx = wave_xor(realign(lds, nibtab, ax)), by = wave_xor(realign(lds, nibtab, ay));
+    if (tx.live()) finish(tx, ex, bx);
+    if (ty.live()) finish(ty, ey, by);
+    if (last) {
+      if (lane < cnt) {
+        if (a.out != nullptr) __builtin_nontemporal_store(res, a.out + first + lane);
+        if (kVerify && a.mismatch != nullptr) __builtin_nontemporal_store((uint8_t)bad, a.mismatch + first + lane);
+      }
+    }
+  };
+
+  // Ring: two pair slots, compile-time slot indices (the loop is unrolled over
+  // them) so no buffer register is copied while its loads are in flight.
+  PTask tk[2][2];
+  uint32_t tfirst[2], tcnt[2], tlast[2];  // per slot: the run's first record, its record count, last pair?
+  uint32_t wb[2][2][kRounds];
+  uint32_t eb[2][2];
+  // records of the next pair to issue (one pair ahead: scalar loads)
+  uint32_t pb = pair_first();
+  SpanRec p0 = read_rec(pb), p1 = read_rec(pb + 1u);
+  auto take = [&](int sl) {
+    const uint32_t b = pb;
+    tk[sl][0] = make(b, p0, lo);
+    tk[sl][1] = make(b + 1u, p1, lo);
+    tfirst[sl] = lo;
+    tcnt[sl] = hi - lo;
+    tlast[sl] = (k < K && b + 2u >= hi) ? 1u : 0u;
+    if (k >= K) {
+      tk[sl][0].f = tk[sl][1].f = 0u;
+      tlast[sl] = 0u;
+    }
+    step();
+    pb = pair_first();
+    p0 = read_rec(pb);
+    p1 = read_rec(pb + 1u);
+  };
+#pragma unroll
+  for (int sl = 0; sl < 2; ++sl) {
+    take(sl);
+    issue(tk[sl][0], wb[sl][0], eb[sl][0]);
+    issue(tk[sl][1], wb[sl][1], eb[sl][1]);
+  }
+  constexpr int kYounger = 2 * (kRounds + 1);  // the other slot's two spans
+  for (;;) {
+#pragma unroll
+    for (int sl = 0; sl < 2; ++sl) {
+      wait_task<kYounger>(wb[sl][0], eb[sl][0]);
+      wait_task<kYounger>(wb[sl][1], eb[sl][1]);
+      if (tk[sl][0].valid())
+        fold(tk[sl][0], wb[sl][0], eb[sl][0], tk[sl][1], wb[sl][1], eb[sl][1], tfirst[sl], tcnt[sl], tlast[sl] != 0u);
+      if (!tk[sl ^ 1][0].valid()) goto drained;
+      take(sl);
+      issue(tk[sl][0], wb[sl][0], eb[sl][0]);
+      issue(tk[sl][1], wb[sl][1], eb[sl][1]);
+    }
+  }
+drained:
+  // the abandoned slot's loads retire while their registers are live
 #pragma unroll
   for (int sl = 0; sl < 2; ++sl) {
     wait_task<0>(wb[sl][0], eb[sl][0]);
@@ -1231,13 +1409,13 @@ hipError_t launch_span(const SpanBatch& a, bool verify, int grid, hipStream_t s)
   // Log records (LOG_HEADER) are short: the variant that skips padding rounds.
   const bool skip = (a.flags & kFlagLogHeader) != 0 && a.role == kRoleSpans;
   if (verify) {
-    if (a.pair_kernel && !skip) crc32c_span_kernel<true, false, true><<<grid, kThreads, 0, s>>>(a);
-    if (skip) crc32c_span_kernel<true, true, false><<<grid, kThreads, 0, s>>>(a);
-    else crc32c_span_kernel<true, false, false><<<grid, kThreads, 0, s>>>(a);
+    if (a.pair_kernel && !skip) crc32c_pair_kernel<true><<<grid, kThreads, 0, s>>>(a);
+    if (skip) crc32c_span_kernel<true, true><<<grid, kThreads, 0, s>>>(a);
+    else crc32c_span_kernel<true, false><<<grid, kThreads, 0, s>>>(a);
   } else {
-    if (a.pair_kernel && !skip) crc32c_span_kernel<false, false, true><<<grid, kThreads, 0, s>>>(a);
-    if (skip) crc32c_span_kernel<false, true, false><<<grid, kThreads, 0, s>>>(a);
-    else crc32c_span_kernel<false, false, false><<<grid, kThreads, 0, s>>>(a);
+    if (a.pair_kernel && !skip) crc32c_pair_kernel<false><<<grid, kThreads, 0, s>>>(a);
+    if (skip) crc32c_span_kernel<false, true><<<grid, kThreads, 0, s>>>(a);
+    else crc32c_span_kernel<false, false><<<grid, kThreads, 0, s>>>(a);
   }
   return hipGetLastError();
 }

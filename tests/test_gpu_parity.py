@@ -229,6 +229,16 @@ def test_pair_run_schedule(dev, oracle, native, n, bulk_route):
     np.testing.assert_array_equal(mm.cpu().numpy(), damaged.astype(np.uint8))
     out2, _ = crc32c.batch(buf, d_off, d_len)  # no init / mask / verify
     np.testing.assert_array_equal(_u32(out2), oracle.batch(host, off, lens.astype(np.uint32))[0])
+    # seal (MASK | WRITE_TRAILER) over zeroed trailers: every trailer is the
+    # masked crc again and no other byte moves
+    sealed = host.copy()
+    sealed[tr] = 0
+    sbuf = torch.from_numpy(sealed).to(dev)
+    out3, _ = crc32c.batch(sbuf, d_off, d_len, d_init, mask=True, trailer=True)
+    np.testing.assert_array_equal(_u32(out3), masked)
+    want = sealed.copy()
+    want[tr] = masked.astype("<u4").view(np.uint8).reshape(-1, 4)
+    np.testing.assert_array_equal(sbuf.cpu().numpy(), want)
 
 
 def test_max_length_span(dev, oracle, native, route):
