@@ -235,6 +235,23 @@ VARIANTS = {
     "lanest_nt": [("crc32c_kernels.hip",
                    '          asm volatile("global_store_dword %0, %1, off" : : "v"(ta), "v"(v) : "memory");\n',
                    '          asm volatile("global_store_dword %0, %1, off nt" : : "v"(ta), "v"(v) : "memory");\n')],
+    # measurement-only bisection of the pair kernel against the fixed kernel
+    # on the same blocks (valid for the sst3988 workload only: 3988-B spans at
+    # stride 3992, init 0): records synthesized from the index, not read
+    "pair_norec": [("crc32c_kernels.hip",
+                    "    if (b < n) r = const_load(a.rec, b);\n    return r;\n  };\n"
+                    "  auto make = [&](uint32_t b, const SpanRec& r, uint32_t first) -> PTask {\n",
+                    "    if (b < n) {\n"
+                    "      const uint64_t ad = reinterpret_cast<uint64_t>(a.base) + 3992ull * b;\n"
+                    "      r.x = (uint32_t)ad;\n      r.y = ((uint32_t)(ad >> 32) & 0xffffu) | (27u << 16);\n"
+                    "      r.z = 3988u;\n      r.w = 0xFFFFFFFFu;\n    }\n    return r;\n  };\n"
+                    "  auto make = [&](uint32_t b, const SpanRec& r, uint32_t first) -> PTask {\n")] + MEASURE_ONLY,
+    # ... and without the edge-byte load (no tail bytes, no verify there)
+    "pair_noedge": [("crc32c_kernels.hip",
+                     "    if (kVerify && lane >= 6u && lane < 10u) eoff = tl + (lane - 6u);\n    e = buf_ubyte(re, eoff);\n  };\n\n  uint32_t res = 0u, bad = 0u;\n",
+                     "    if (kVerify && lane >= 6u && lane < 10u) eoff = tl + (lane - 6u);\n    (void)eoff;\n    e = 0u;\n  };\n\n  uint32_t res = 0u, bad = 0u;\n"),
+                    ("crc32c_kernels.hip", "  constexpr int kYounger = 2 * (kRounds + 1);  // the other slot's two spans\n",
+                     "  constexpr int kYounger = 2 * kRounds;  // the other slot's two spans\n")] + MEASURE_ONLY,
     # 16 waves per CU with the ticket path folding one chunk per step (its
     # two-chunk steps held 64 VGPRs): does the kernel then fit 128 VGPRs, and
     # do shorter runs per wave (~4 spans of a file instead of ~5.5) pay?
@@ -464,6 +481,10 @@ def do_run(args, names):
                      int(hlen.sum() + len(hlen)) * nf + nw * (4 + 4 + 12)),
         "sst3988": (lambda n: libs[n][1](buf.data_ptr(), soff.data_ptr(), slen.data_ptr(), None, ns,
                                          sout.data_ptr(), None, 0, sp), ns * (3988 + 4 + 12)),
+        # the same blocks through the fixed kernel (stride 3992, 3988 B; bytes
+        # counted as for sst3988, so the rates compare as times)
+        "sst3988_fixed": (lambda n: libs[n][0](buf.data_ptr(), 3992, 3988, ns, 0, sout.data_ptr(), None, 0, sp),
+                          ns * (3988 + 4 + 12)),
         # the same spans sealed (MASK | WRITE_TRAILER): the planner path's trailer stores
         "sst3988_seal": (lambda n: libs[n][1](buf.data_ptr(), soff.data_ptr(), slen.data_ptr(), None, ns,
                                               sout.data_ptr(), None, 0x3, sp), ns * (3988 + 4 + 12)),
@@ -521,7 +542,7 @@ def do_run(args, names):
         work = {w: v for w, v in work.items() if w in args.work}
     res = {w: {n: [] for n in names} for w in work}
     agree = {}
-    outs_of = {"wal": wout, "wal_seal": wout, "sst3988": sout, "sst3988_seal": sout, "huge64m": hout, "one_huge": hout, "file_fixed": fout,
+    outs_of = {"wal": wout, "wal_seal": wout, "sst3988": sout, "sst3988_seal": sout, "sst3988_fixed": sout, "huge64m": hout, "one_huge": hout, "file_fixed": fout,
                "file_desc": fout, "file_seal": fout, "files7_seal": f7out, "files7_verify": f7out, "files2_seal": f7out,
                "files2_verify": f7out, "files3_seal": f7out, "files3_verify": f7out,
                "file_verify": fout, "tiny_desc": fout}
