@@ -252,6 +252,29 @@ VARIANTS = {
                      "    if (kVerify && lane >= 6u && lane < 10u) eoff = tl + (lane - 6u);\n    (void)eoff;\n    e = 0u;\n  };\n\n  uint32_t res = 0u, bad = 0u;\n"),
                     ("crc32c_kernels.hip", "  constexpr int kYounger = 2 * (kRounds + 1);  // the other slot's two spans\n",
                      "  constexpr int kYounger = 2 * kRounds;  // the other slot's two spans\n")] + MEASURE_ONLY,
+    # measurement-only bisection, continued: the pair kernel's live spans with
+    # 0 < pad <= 64 read through the fixed kernel's global loads (SGPR base,
+    # round 0 clamped to the body start and masked in the fold) instead of
+    # range-checked buffer loads
+    "pair_gload": [("crc32c_kernels.hip",
+                    "    } else if (pad <= 64u) {\n      w[0] = buf_dword<0>(rb, (uint32_t)i0 * 4u);\n"
+                    "      load_rounds_from1(w, rb, (uint32_t)(i0 + 64) * 4u);\n    } else {\n#pragma unroll\n"
+                    "      for (int j = 0; j < kRounds; ++j) w[j] = buf_dword<0>(rb, (uint32_t)(i0 + 64 * j) * 4u);\n"
+                    "    }\n    uint32_t eoff = 0xFFFFFFFFu;\n    if (lane >= 3u && lane < 3u + tl) eoff = lane - 3u;",
+                    "    } else if (live && pad <= 64u) {\n"
+                    "      const uint8_t* bp = reinterpret_cast<const uint8_t*>(t.body);\n"
+                    "      w[0] = asm_load_dword<0>(bp, i0 < 0 ? 0u : (uint32_t)i0 * 4u);\n"
+                    "      const uint32_t off1 = (uint32_t)(i0 + 64) * 4u;\n#pragma unroll\n"
+                    "      for (int j = 1; j < kRounds; ++j) w[j] = asm_load_dword_at<kRounds>(bp, off1, j);\n"
+                    "    } else if (pad <= 64u) {\n      w[0] = buf_dword<0>(rb, (uint32_t)i0 * 4u);\n"
+                    "      load_rounds_from1(w, rb, (uint32_t)(i0 + 64) * 4u);\n    } else {\n#pragma unroll\n"
+                    "      for (int j = 0; j < kRounds; ++j) w[j] = buf_dword<0>(rb, (uint32_t)(i0 + 64 * j) * 4u);\n"
+                    "    }\n    uint32_t eoff = 0xFFFFFFFFu;\n    if (lane >= 3u && lane < 3u + tl) eoff = lane - 3u;"),
+                   ("crc32c_kernels.hip",
+                    "    if (lx) inject(tx, wx);\n    if (ly) inject(ty, wy);\n",
+                    "    if (tx.live() && tx.pad() <= 64u) wx[0] = lane >= tx.pad() ? wx[0] : 0u;\n"
+                    "    if (ty.live() && ty.pad() <= 64u) wy[0] = lane >= ty.pad() ? wy[0] : 0u;\n"
+                    "    if (lx) inject(tx, wx);\n    if (ly) inject(ty, wy);\n")] + MEASURE_ONLY,
     # 16 waves per CU with the ticket path folding one chunk per step (its
     # two-chunk steps held 64 VGPRs): does the kernel then fit 128 VGPRs, and
     # do shorter runs per wave (~4 spans of a file instead of ~5.5) pay?
