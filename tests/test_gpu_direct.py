@@ -122,6 +122,32 @@ def test_sst_files_verify_damaged(dev, oracle, native, files):
     np.testing.assert_array_equal(_u32(out2), want2)
 
 
+@pytest.mark.parametrize("files", [1, 7])
+def test_sst_files_seal_zeroed_trailers(dev, oracle, native, files):
+    """WriteRawBlock over one and seven files per call into zeroed trailers
+    (the ring spans' non-temporal trailer stores, the index block's through
+    its tickets): every trailer is the masked crc again and no other byte of
+    the buffer moves."""
+    import torch
+    from prismdb_amd import crc32c
+
+    host, off, lens, raw, masked = _sst_file(oracle, 0x5EED00D4 + files, files)
+    n = len(off)
+    tr = (off + lens.astype(np.uint64)).astype(np.int64)[:, None] + np.arange(4)[None, :]
+    zeroed = host.copy()
+    zeroed[tr] = 0
+    buf = torch.from_numpy(zeroed).to(dev)
+    d_off = torch.from_numpy(off.astype(np.int64)).to(dev)
+    d_len = torch.from_numpy(lens.view(np.int32)).to(dev)
+    out, _ = crc32c.batch(buf, d_off, d_len, mask=True, trailer=True)
+    assert _last_split_rc(native) == -2
+    np.testing.assert_array_equal(_u32(out), masked)
+    got = buf.cpu().numpy()
+    np.testing.assert_array_equal(got[tr], host[tr])
+    assert (got == host).all()
+    assert n == files * (ND + 1)
+
+
 RING_CHUNKS = 32  # kRingChunks: spans of up to 32 chunks of 4 KiB are folded in the static ring
 TICKET_LG_MIN = 2  # kTicketLgMin
 
