@@ -79,6 +79,10 @@ def parse():
                     help="config-5 compaction legs: SST files per leveldb_crc32c_batch call (comma list; 7 files "
                          "are the most one launch takes, 12 a compaction's input set: 1 file + ~11 overlapping)")
     ap.add_argument("--no-multi", action="store_true", help="skip the one-process batch_multi leg")
+    ap.add_argument("--multi-timeout", type=float, default=240.0,
+                    help="seconds the batch_multi leg's child process may take before it is stopped")
+    ap.add_argument("--multi-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--multi-devices", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--cpu-all-blocks", type=int, default=1 << 20,
                     help="cpu_baseline all-cores figure: blocks (config 1: 1 Mi x 4 KiB)")
     return ap.parse_args()
@@ -576,8 +580,41 @@ def spawn_ranks(args) -> int:
     return subprocess.call(cmd, env=env)
 
 
+def run_multi_child(args, ndev: int) -> dict:
+    """The batch_multi leg in a child process of its own, under a time limit:
+    it drives every device through one RCCL clique, and a hang or a fault
+    there must not cost the line whose headline was already measured.  (A
+    child process, not an exec: this process has initialised the GPU.)"""
+    cmd = [sys.executable, os.path.abspath(__file__), "--multi-child", "--multi-devices", str(ndev),
+           "--c5-spans", str(args.c5_spans), "--c5-steps", str(args.c5_steps)]
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "MASTER_PORT")}
+    try:
+        r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=args.multi_timeout)
+    except subprocess.TimeoutExpired:
+        return {"devices": ndev, "error": f"batch_multi leg stopped after {args.multi_timeout:.0f} s"}
+    for line in reversed(r.stdout.splitlines()):
+        if line.startswith("{"):
+            try:
+                return json.loads(line)
+            except ValueError:
+                break
+    return {"devices": ndev, "error": f"batch_multi child exited {r.returncode}: {r.stderr.strip()[-400:]}"}
+
+
 def main() -> int:
     args = parse()
+    if args.multi_child:  # bench's own child (run_multi_child): the batch_multi leg alone
+        import torch
+
+        from prismdb_amd import crc32c
+
+        try:
+            res = multi_leg(args, torch, crc32c, args.multi_devices)
+        except Exception as e:
+            res = {"devices": args.multi_devices, "error": f"{type(e).__name__}: {e}"}
+        print(json.dumps(res), flush=True)
+        return 0
     # The launch mode is settled before anything touches the GPU.
     if os.environ.get("WORLD_SIZE") is None and args.gpus > 1:
         return spawn_ranks(args)
@@ -686,17 +723,16 @@ def main() -> int:
         c5 = config5_leg(args, torch, dist, crc32c, dev, rank, world)
     multi = None
     if not args.no_multi:
-        # rank 0 alone drives all `world` devices; the others free their
-        # memory and wait on the host
+        # one child process of rank 0 drives the devices (all `world` ranks'
+        # devices; at world 1 every visible device, PrismDB's one-process
+        # shape); the ranks free their memory and wait on the host
         del outs
         torch.cuda.empty_cache()
         if world > 1:
             dist.barrier(group=cpu_group)
         if rank == 0:
-            try:
-                multi = multi_leg(args, torch, crc32c, world)
-            except Exception as e:  # reported in the line; the headline stands on its own
-                multi = {"devices": world, "error": f"{type(e).__name__}: {e}"}
+            ndev = world if world > 1 else max(1, min(8, torch.cuda.device_count()))
+            multi = run_multi_child(args, ndev)
         if world > 1:
             dist.barrier(group=cpu_group)
 

@@ -67,3 +67,30 @@ def test_gpus_2_without_devices_fails_loudly():
     assert r.returncode != 0
     assert '"n_gpus": 1' not in r.stdout
     assert all("n_gpus" not in d for d in _json_lines(r.stdout))
+
+
+def _bench_module():
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("bench_under_test", BENCH)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def test_multi_leg_child_reports_instead_of_raising(monkeypatch):
+    """The batch_multi leg runs in a child process under a time limit; a child
+    that fails (no device here) or runs out of time comes back as an `error`
+    entry for the line, never as an exception or a hang of the bench."""
+    import torch
+
+    if torch.cuda.device_count() > 0:
+        pytest.skip("devices visible: this checks the failure paths")
+    bench = _bench_module()
+    monkeypatch.setattr(sys, "argv", [BENCH, "--c5-spans", "1000", "--c5-steps", "1"])
+    args = bench.parse()
+    res = bench.run_multi_child(args, 1)
+    assert res["devices"] == 1 and "error" in res
+    args.multi_timeout = 0.01
+    res = bench.run_multi_child(args, 2)
+    assert res == {"devices": 2, "error": "batch_multi leg stopped after 0 s"}
