@@ -720,7 +720,13 @@ def main() -> int:
     torch.cuda.empty_cache()
     c5 = None
     if not args.no_config5:
-        c5 = config5_leg(args, torch, dist, crc32c, dev, rank, world)
+        if world == 1:
+            try:  # one rank: a failure here is reported in the line, the headline stands
+                c5 = config5_leg(args, torch, dist, crc32c, dev, rank, world)
+            except Exception as e:
+                c5 = {"error": f"{type(e).__name__}: {e}"}
+        else:  # (ranks meet in collectives inside: one rank's exception must end them all)
+            c5 = config5_leg(args, torch, dist, crc32c, dev, rank, world)
     multi = None
     if not args.no_multi:
         # one child process of rank 0 drives the devices (all `world` ranks'
