@@ -91,6 +91,18 @@ def main():
                len(lens))
         res["config3_mixed_windows"]["agrees"] = bool(torch.equal(ref, out))
         del d_off, d_len, out
+    if want("config3_seal"):
+        # the same span sizes sealed (MASK | WRITE_TRAILER): a 4-B trailer slot after each span
+        off = np.concatenate([[0], np.cumsum(lens + 4)[:-1]])
+        d_off, d_len = torch.from_numpy(off).to(dev), torch.from_numpy(lens.astype(np.int32)).to(dev)
+        out = torch.empty(len(lens), dtype=torch.int32, device=dev)
+        fn = lambda: crc32c.batch(buf, d_off, d_len, out=out, mask=True, trailer=True, check_bounds=False)  # noqa: E731
+        report("config3_seal", timed(fn, args.reps), lens.sum(), lens.sum() + 20 * len(lens), len(lens))
+        ref = out.clone()
+        report("config3_seal_windows", timed(windows(fn), args.reps), lens.sum(), lens.sum() + 20 * len(lens),
+               len(lens))
+        res["config3_seal_windows"]["agrees"] = bool(torch.equal(ref, out))
+        del d_off, d_len, out
 
     # SST-shaped, fixed stride
     n = 1 << 24
@@ -123,6 +135,12 @@ def main():
         ref = out2.clone()
         report("sst_desc_windows", timed(windows(fn), args.reps), lens.sum(), lens.sum() + 16 * len(lens), len(lens))
         res["sst_desc_windows"]["agrees"] = bool(torch.equal(ref, out2))
+        # WriteRawBlock over the same blocks (MASK | WRITE_TRAILER into the trailer slots)
+        fs = lambda: crc32c.batch(buf, d_off, d_len, out=out2, mask=True, trailer=True, check_bounds=False)  # noqa: E731
+        report("sst_seal", timed(fs, args.reps), lens.sum(), lens.sum() + 20 * len(lens), len(lens))
+        ref = out2.clone()
+        report("sst_seal_windows", timed(windows(fs), args.reps), lens.sum(), lens.sum() + 20 * len(lens), len(lens))
+        res["sst_seal_windows"]["agrees"] = bool(torch.equal(ref, out2))
         del d_off, d_len, out2
 
     # verify 4 KiB spans (fixed stride 4096, span 4092 B, trailer in the last 4 B)
