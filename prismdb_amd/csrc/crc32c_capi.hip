@@ -43,6 +43,7 @@ thread_local std::string t_last_error;
 thread_local const prismdb::dev::SplitCounters* t_last_counters = nullptr;
 thread_local hipStream_t t_last_stream = nullptr;
 thread_local bool t_last_direct = false;
+thread_local bool t_last_pair = false;  // the planner batch launched the pair-run kernel
 thread_local const uint32_t* t_last_stats = nullptr;
 
 int Fail(int code, const std::string& msg) {
@@ -658,6 +659,7 @@ int RunBatch(DeviceCtx& ctx, const SpanBatch& base_args, bool desc, bool verify,
                           !(a.flags & prismdb::dev::kFlagLogHeader)
                       ? 1u
                       : 0u;
+  t_last_pair = a.pair_kernel != 0u;
   e = prismdb::dev::launch_span(a, verify, ctx.cus, s);
   if (e != hipSuccess) return FailHip(e, "span kernel launch");
   SpanBatch seg{};
@@ -868,6 +870,24 @@ int prismdb_crc32c_last_split(uint64_t out[4]) {
   out[1] = c.nseg;
   out[2] = c.overflow;
   out[3] = c.nlist;
+  return 0;
+}
+
+// Test hook: the span pass's schedule of this thread's last planner-path
+// batch: out[0] = chunk tasks, out[1] = task-balanced slices (0: every record
+// one task -- the pair-run kernel's schedule when the host launched it),
+// out[2] = 1 if the host launched the pair-run kernel.  -2 after a one-launch
+// batch, -1 before any planner batch.
+int prismdb_crc32c_last_schedule(uint64_t out[3]) {
+  if (t_last_direct) return -2;
+  if (t_last_counters == nullptr) return -1;
+  prismdb::dev::SplitCounters c{};
+  hipError_t e = hipStreamSynchronize(t_last_stream);
+  if (e == hipSuccess) e = hipMemcpy(&c, t_last_counters, sizeof(c), hipMemcpyDeviceToHost);
+  if (e != hipSuccess) return FailHip(e, "prismdb_crc32c_last_schedule");
+  out[0] = c.tasks;
+  out[1] = c.nslices;
+  out[2] = t_last_pair ? 1u : 0u;
   return 0;
 }
 

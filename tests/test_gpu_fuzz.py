@@ -189,6 +189,10 @@ def test_random_pair_batches(dev, oracle, native, seed, planner_bulk):
     arr = (ctypes.c_uint64 * 4)()
     native.prismdb_crc32c_last_split.argtypes = [ctypes.c_void_p]
     assert native.prismdb_crc32c_last_split(arr) == 0 and arr[2] == 0
+    sched = (ctypes.c_uint64 * 3)()
+    native.prismdb_crc32c_last_schedule.argtypes = [ctypes.c_void_p]
+    assert native.prismdb_crc32c_last_schedule(sched) == 0
+    assert sched[1] == 0 and sched[2] == 1, list(sched)  # the pair-run kernel took the batch
     np.testing.assert_array_equal(_u32(out), want)
     if verify:
         raw, _ = oracle.batch(host, off, lens, init)

@@ -1,6 +1,8 @@
 """Parity of the MI355X engine against the oracle and the reference's golden
 outputs.  Bit-exact (integer path).  All calls go through the C ABI
 (prismdb_amd.crc32c -> libprismdb_crc32c.so)."""
+import ctypes
+
 import numpy as np
 import pytest
 
@@ -225,6 +227,13 @@ def test_pair_run_schedule(dev, oracle, native, n, bulk_route):
     d_len = torch.from_numpy(lens.astype(np.uint32).view(np.int32)).to(dev)
     d_init = torch.from_numpy(init.view(np.int32)).to(dev)
     out, mm = crc32c.batch(buf, d_off, d_len, d_init, mask=True, verify=True)
+    sched = (ctypes.c_uint64 * 3)()
+    native.prismdb_crc32c_last_schedule.argtypes = [ctypes.c_void_p]
+    rc = native.prismdb_crc32c_last_schedule(sched)
+    if bulk_route == "planner":  # every record one task: the pair-run kernel's schedule, and it was launched
+        assert rc == 0 and sched[0] == n and sched[1] == 0 and sched[2] == 1, (rc, list(sched))
+    else:
+        assert rc == -2  # windows of the one-launch kernel
     np.testing.assert_array_equal(_u32(out), masked)
     np.testing.assert_array_equal(mm.cpu().numpy(), damaged.astype(np.uint8))
     out2, _ = crc32c.batch(buf, d_off, d_len)  # no init / mask / verify
