@@ -40,50 +40,6 @@ VARIANTS = {
     "base": [],
     # an identical copy under another name: A/A check of the harness
     "base2": [],
-    # measurement-only (wrong results): the one-launch kernel without its LDS
-    # table fill -- what the fill costs a file-sized call
-    "direct_notables": [("crc32c_direct.hip", "    load_tables<kDirectThreads>(lds, a.tabs, tid);\n", "")]
-    + MEASURE_ONLY,
-    # measurement-only (wrong results): the static ring without the table fold
-    # (loads, edges and stores only) -- what the fold costs
-    "direct_nofold": [("crc32c_direct.hip",
-                       "          for (int st = 0; st < 3; ++st) acc[st] = step256(lds, tab, acc[st], w[st][j]);",
-                       "          for (int st = 0; st < 3; ++st) acc[st] ^= w[st][j];")] + MEASURE_ONLY,
-    # measurement-only (leaks workspaces at thread exit): no event recorded
-    # after each batch -- what the per-call hipEventRecord costs
-    "noevent": [("crc32c_capi.hip", "    ~MarkDone() { (void)hipEventRecord(w->done, s); }\n", "    ~MarkDone() {}\n")]
-    + MEASURE_ONLY,
-    # the one-launch kernel's completion marks the workspace event through
-    # hipExtLaunchKernel's stop event (no separate marker packet)
-    "extstop": [
-        ("crc32c_device.h",
-         "hipError_t launch_direct(const SpanBatch& a, bool verify, int grid, const DirectWs& d, hipStream_t s);",
-         "hipError_t launch_direct(const SpanBatch& a, bool verify, int grid, const DirectWs& d, hipStream_t s,\n"
-         "                         hipEvent_t done);"),
-        ("crc32c_direct.hip",
-         "hipError_t launch_direct(const SpanBatch& a, bool verify, int grid, const DirectWs& d, hipStream_t s) {\n"
-         "  if (verify) crc32c_direct_kernel<true><<<grid, kDirectThreads, 0, s>>>(a, d);\n"
-         "  else crc32c_direct_kernel<false><<<grid, kDirectThreads, 0, s>>>(a, d);\n",
-         "hipError_t launch_direct(const SpanBatch& a, bool verify, int grid, const DirectWs& d, hipStream_t s,\n"
-         "                         hipEvent_t done) {\n"
-         "  if (verify) hipExtLaunchKernelGGL(crc32c_direct_kernel<true>, dim3(grid), dim3(kDirectThreads), 0, s, nullptr, done, 0u, a, d);\n"
-         "  else hipExtLaunchKernelGGL(crc32c_direct_kernel<false>, dim3(grid), dim3(kDirectThreads), 0, s, nullptr, done, 0u, a, d);\n"),
-        ("crc32c_direct.hip", '#include "crc32c_fold.h"\n', '#include "crc32c_fold.h"\n#include <hip/hip_ext.h>\n'),
-        ("crc32c_capi.hip", "    ~MarkDone() { (void)hipEventRecord(w->done, s); }\n",
-         "    bool ext = false;\n    ~MarkDone() { if (!ext) (void)hipEventRecord(w->done, s); }\n"),
-        ("crc32c_capi.hip", "    hipError_t e = prismdb::dev::launch_direct(a, verify, ctx.cus, d, s);\n",
-         "    mark.ext = true;\n    hipError_t e = prismdb::dev::launch_direct(a, verify, ctx.cus, d, s, w->done);\n"),
-    ],
-    # the one-launch kernel's table words retired before slot 0 is issued
-    # (slot 0's loads then do not queue the table loads behind them)
-    "tables_first": [("crc32c_direct.hip",
-                      "#pragma unroll\n    for (int st = 0; st < 3; ++st) issue(tk[0][st], wb[0][st], eb[0][st]);\n"
-                      "    tables_wait<3 * (kRounds + 1)>(tr);  // slot 0's 51 loads stay in flight\n",
-                      "    tables_wait<0>(tr);\n"
-                      "#pragma unroll\n    for (int st = 0; st < 3; ++st) issue(tk[0][st], wb[0][st], eb[0][st]);\n")],
-    # tickets of one chunk (a 486 977-B index span: 119 tickets instead of 60)
-    "lg0": [("crc32c_direct.hip", "  return per <= 1u ? 0u : (per <= 2u ? 1u : (per <= 4u ? 2u : 3u));",
-             "  return 0u * per;")],
     # twice the ticket workers (nwaves / 16)
     "workers2x": [("crc32c_direct.hip", "  uint32_t reserve = nwaves / 32u;", "  uint32_t reserve = nwaves / 16u;")],
     # measurement-only (wrong results: no header written): the lane kernel
@@ -91,22 +47,6 @@ VARIANTS = {
     "lane_noseal": [("crc32c_kernels.hip",
                      '          asm volatile("global_store_dword %0, %1, off" : : "v"(ta), "v"(v) : "memory");\n',
                      '          (void)ta;\n')] + MEASURE_ONLY,
-    # the one-launch kernel's table fill retired after slot 0's first task
-    # only (17 loads in flight), the group barrier before the other two
-    # tasks of slot 0 are issued: issuing all 51 first held the barrier until
-    # the memory system had drained ~37 MB (~5 us)
-    "tables_after_st0": [("crc32c_direct.hip",
-                          "#pragma unroll\n    for (int st = 0; st < 3; ++st) issue(tk[0][st], wb[0][st], eb[0][st]);\n"
-                          "    tables_wait<3 * (kRounds + 1)>(tr);  // slot 0's 51 loads stay in flight\n"
-                          "    tables_store<kDirectThreads>(lds, tr, tid);\n"
-                          "    // Group barrier for the LDS image.  Not __syncthreads(): its release\n"
-                          "    // fence waits for every outstanding load (vmcnt(0)), slot 0's included.\n"
-                          "    asm volatile(\"s_waitcnt lgkmcnt(0)\\n\\ts_barrier\" ::: \"memory\");\n",
-                          "    issue(tk[0][0], wb[0][0], eb[0][0]);\n"
-                          "    tables_wait<kRounds + 1>(tr);\n"
-                          "    tables_store<kDirectThreads>(lds, tr, tid);\n"
-                          "    asm volatile(\"s_waitcnt lgkmcnt(0)\\n\\ts_barrier\" ::: \"memory\");\n"
-                          "#pragma unroll\n    for (int st = 1; st < 3; ++st) issue(tk[0][st], wb[0][st], eb[0][st]);\n")],
     # the sealing lane kernel's side load of a record's last task reads the
     # dword holding its header crc (unused: HD is only read at task 0), so
     # that the line is in L2 when the crc is stored
@@ -153,14 +93,6 @@ VARIANTS = {
          "                 lane == 5 ? ts5 : lane == 6 ? (uint64_t)m : tsw;\n"
          "    reinterpret_cast<uint64_t*>(a.out + ((n + 3u) & ~3u))[8u * wave + lane] = v;\n  }\n}\n\nhipError_t launch_direct"),
     ] + MEASURE_ONLY,
-    # the one-launch kernel's slot 1 issued only once slot 0 has landed: the
-    # memory system then serves every wave's first three tasks first (37 MB)
-    # instead of interleaving all 67 MB of a file, and slot 0's folds overlap
-    # slot 1's loads instead of all folds bunching at the end
-    "slot1_late": [("crc32c_direct.hip",
-                    "        // slot 0 went out before the table fill; slot 1 now\n",
-                    "        // slot 0 went out before the table fill; slot 1 once it has landed\n"
-                    "#pragma unroll\n        for (int st = 0; st < 3; ++st) wait_task<0>(wb[0][st], eb[0][st]);\n")],
     # the one-launch kernel before round 4's ring change: two slots of three
     # streams (tools/patches/crc32c_direct_r03.hip, the round-3 source)
     "ring6": [("crc32c_direct.hip", "@file", "tools/patches/crc32c_direct_r03.hip")],
@@ -214,15 +146,6 @@ VARIANTS = {
                  "                       \"global_store_dwordx4 %0, %1, off offset:96\\n\\tglobal_store_dwordx4 %0, %1, off offset:112\"\n"
                  "                       : : \"v\"(ta), \"v\"(vv) : \"memory\");\n"
                  "        }\n")] + MEASURE_ONLY,
-    # trailer stores with other cache policies: sc1 / sc0 sc1 write through
-    # and drop the line from the XCD's L2, nt streams it -- so the dirty
-    # sectors leave during the kernel instead of at its end-of-kernel write-back?
-    "st_sc1": [("crc32c_fold.h", '  asm volatile("global_store_dword %0, %1, off" : : "v"(p), "v"(v) : "memory");\n',
-                '  asm volatile("global_store_dword %0, %1, off sc1" : : "v"(p), "v"(v) : "memory");\n')],
-    "st_sc0sc1": [("crc32c_fold.h", '  asm volatile("global_store_dword %0, %1, off" : : "v"(p), "v"(v) : "memory");\n',
-                '  asm volatile("global_store_dword %0, %1, off sc0 sc1" : : "v"(p), "v"(v) : "memory");\n')],
-    "st_nt": [("crc32c_fold.h", '  asm volatile("global_store_dword %0, %1, off" : : "v"(p), "v"(v) : "memory");\n',
-                '  asm volatile("global_store_dword %0, %1, off nt" : : "v"(p), "v"(v) : "memory");\n')],
     # the lane kernel's 128-B line loads non-temporal (round 2 measured nt
     # halving the v2 kernel, whose tasks straddled lines; v3's are line-aligned)
     "lane_nt": [("crc32c_kernels.hip",
@@ -252,29 +175,6 @@ VARIANTS = {
                      "    if (kVerify && lane >= 6u && lane < 10u) eoff = tl + (lane - 6u);\n    (void)eoff;\n    e = 0u;\n  };\n\n  uint32_t res = 0u, bad = 0u;\n"),
                     ("crc32c_kernels.hip", "  constexpr int kYounger = 2 * (kRounds + 1);  // the other slot's two spans\n",
                      "  constexpr int kYounger = 2 * kRounds;  // the other slot's two spans\n")] + MEASURE_ONLY,
-    # measurement-only bisection, continued: the pair kernel's live spans with
-    # 0 < pad <= 64 read through the fixed kernel's global loads (SGPR base,
-    # round 0 clamped to the body start and masked in the fold) instead of
-    # range-checked buffer loads
-    "pair_gload": [("crc32c_kernels.hip",
-                    "    } else if (pad <= 64u) {\n      w[0] = buf_dword<0>(rb, (uint32_t)i0 * 4u);\n"
-                    "      load_rounds_from1(w, rb, (uint32_t)(i0 + 64) * 4u);\n    } else {\n#pragma unroll\n"
-                    "      for (int j = 0; j < kRounds; ++j) w[j] = buf_dword<0>(rb, (uint32_t)(i0 + 64 * j) * 4u);\n"
-                    "    }\n    uint32_t eoff = 0xFFFFFFFFu;\n    if (lane >= 3u && lane < 3u + tl) eoff = lane - 3u;",
-                    "    } else if (live && pad <= 64u) {\n"
-                    "      const uint8_t* bp = reinterpret_cast<const uint8_t*>(t.body);\n"
-                    "      w[0] = asm_load_dword<0>(bp, i0 < 0 ? 0u : (uint32_t)i0 * 4u);\n"
-                    "      const uint32_t off1 = (uint32_t)(i0 + 64) * 4u;\n#pragma unroll\n"
-                    "      for (int j = 1; j < kRounds; ++j) w[j] = asm_load_dword_at<kRounds>(bp, off1, j);\n"
-                    "    } else if (pad <= 64u) {\n      w[0] = buf_dword<0>(rb, (uint32_t)i0 * 4u);\n"
-                    "      load_rounds_from1(w, rb, (uint32_t)(i0 + 64) * 4u);\n    } else {\n#pragma unroll\n"
-                    "      for (int j = 0; j < kRounds; ++j) w[j] = buf_dword<0>(rb, (uint32_t)(i0 + 64 * j) * 4u);\n"
-                    "    }\n    uint32_t eoff = 0xFFFFFFFFu;\n    if (lane >= 3u && lane < 3u + tl) eoff = lane - 3u;"),
-                   ("crc32c_kernels.hip",
-                    "    if (lx) inject(tx, wx);\n    if (ly) inject(ty, wy);\n",
-                    "    if (tx.live() && tx.pad() <= 64u) wx[0] = lane >= tx.pad() ? wx[0] : 0u;\n"
-                    "    if (ty.live() && ty.pad() <= 64u) wy[0] = lane >= ty.pad() ? wy[0] : 0u;\n"
-                    "    if (lx) inject(tx, wx);\n    if (ly) inject(ty, wy);\n")] + MEASURE_ONLY,
     # 16 waves per CU with the ticket path folding one chunk per step (its
     # two-chunk steps held 64 VGPRs): does the kernel then fit 128 VGPRs, and
     # do shorter runs per wave (~4 spans of a file instead of ~5.5) pay?
@@ -332,11 +232,6 @@ VARIANTS = {
         ("crc32c_kernels.hip", '    asm volatile("" : "+v"(HD[sl]), "+v"(ED[sl]), "+v"(SC[sl]));\n',
          '    asm volatile("" : "+v"(HD[sl]), "+v"(ED[sl]), "+v"(SC[sl]), "+v"(SA[sl]), "+v"(SB[sl]));\n'),
     ],
-    # trailers as four byte stores (before round 4: one dword store)
-    "bytestores": [("crc32c_fold.h",
-                    '  asm volatile("global_store_dword %0, %1, off" : : "v"(p), "v"(v) : "memory");\n',
-                    "  uint8_t* q = const_cast<uint8_t*>(p);\n  q[0] = (uint8_t)v;\n  q[1] = (uint8_t)(v >> 8);\n"
-                    "  q[2] = (uint8_t)(v >> 16);\n  q[3] = (uint8_t)(v >> 24);\n")],
 }
 
 # the previous commit's kernels (a git worktree under build/:
@@ -364,8 +259,6 @@ VARIANTS["walsafe"] = [
      "      }\n"),
 ]
 # combinations
-VARIANTS["tf_ts"] = VARIANTS["tables_first"] + VARIANTS["direct_ts"]
-VARIANTS["tf_lg0_w2"] = VARIANTS["tables_first"] + VARIANTS["lg0"] + VARIANTS["workers2x"]
 
 
 def do_build(names):
