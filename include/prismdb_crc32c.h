@@ -109,7 +109,7 @@ int leveldb_crc32c_batch(const void* dev_base, const uint64_t* dev_off, const ui
  * Host-resident batch (blocks still in host memory, e.g. SST pages read by
  * pread during compaction): span i = host_base[off[i], off[i] + len[i]),
  * offsets sorted ascending, each span (+ its 4-byte trailer when verifying)
- * at most 64 MiB.  Streams 32 MiB chunks host -> device (through pinned
+ * at most 64 MiB.  Streams 64 MiB chunks host -> device (through pinned
  * staging when host_base is pageable; directly when it is pinned/registered)
  * -> batch kernel -> results back, four chunks in flight on the engine's own
  * streams.  Synchronous; out/mismatch are host arrays (either may be NULL).

@@ -71,6 +71,7 @@ def _declare(lib: ctypes.CDLL) -> None:
         "prismdb_crc32c_direct_max": (u64, [u64]),
         "prismdb_crc32c_last_split": (ctypes.c_int, [vp]),
         "prismdb_crc32c_last_schedule": (ctypes.c_int, [vp]),
+        "prismdb_pipeline_chunk_bytes": (ctypes.c_size_t, [ctypes.c_size_t]),
         "prismdb_crc32c_direct_tickets": (u32, [u32]),
         "prismdb_crc32c_direct_debug": (u32, [u32]),
         "prismdb_crc32c_direct_stats": (ctypes.c_int, [vp]),

@@ -41,7 +41,10 @@ void ReleaseEngineStream(hipStream_t s);
 
 namespace {
 
-constexpr size_t kChunkBytes = 32ull << 20;  // per DMA; ~0.6 ms of PCIe Gen5 x16
+// per DMA (~1.2 ms of PCIe Gen5 x16), the slot size: 2 GiB of 4 KiB blocks
+// stream at 51.7 GiB/s pinned / 50.7 pageable against 50.9 / 50.2 with
+// 32 MiB chunks and 53.6 for the plain copy (profiles/r04/r04aa_pipe_chunks.json)
+constexpr size_t kChunkBytes = 64ull << 20;
 constexpr size_t kMaxSpan = 64ull << 20;     // one 64 MiB SST (include/leveldb/options.h:117)
 constexpr size_t kSlotBytes = kMaxSpan + 8;  // a chunk holds one span of up to kMaxSpan
 constexpr size_t kChunkSpans = 1u << 16;     // descriptors per chunk
@@ -53,6 +56,10 @@ constexpr int kMaxDevices = 64;
 // the k-th chunk of every later call fails as a device error would, after the
 // earlier chunks have been enqueued.  0 = off.
 std::atomic<int> g_fail_after_chunks{0};
+// Chunk size (tuning hook prismdb_pipeline_chunk_bytes; default kChunkBytes):
+// spans are packed into chunks of at most this many bytes (a single span may
+// be larger, up to kMaxSpan, the slot size).
+std::atomic<size_t> g_chunk_bytes{kChunkBytes};
 
 int PipeFail(int code, const std::string& msg) {
   prismdb::SetLastError(msg);
@@ -287,11 +294,12 @@ int leveldb_crc32c_batch_host(const void* host_base, const uint64_t* off, const 
     // Chunk: consecutive spans whose bytes (plus trailers) fit kChunkBytes;
     // a single span may be larger (up to kMaxSpan).
     const uint64_t lo = off[i] - lead;
+    const uint64_t chunk_bytes = g_chunk_bytes.load(std::memory_order_relaxed);
     uint64_t hi = lo;
     size_t j = i;
     while (j < n && j - i < kChunkSpans) {
       const uint64_t end = std::max<uint64_t>(hi, off[j] + len[j] + tail);
-      if (j > i && end - lo > kChunkBytes) break;
+      if (j > i && end - lo > chunk_bytes) break;
       hi = end;
       ++j;
     }
@@ -343,5 +351,13 @@ int leveldb_crc32c_batch_host(const void* host_base, const uint64_t* off, const 
 }
 
 void prismdb_pipeline_fail_after(int chunks) { g_fail_after_chunks.store(chunks > 0 ? chunks : 0, std::memory_order_relaxed); }
+
+// Tuning hook: chunk size of later host batches (0: leave it; clamped to
+// [1 MiB, kMaxSpan]); returns the previous value.
+size_t prismdb_pipeline_chunk_bytes(size_t bytes) {
+  if (bytes == 0) return g_chunk_bytes.load(std::memory_order_relaxed);
+  const size_t b = bytes < (1u << 20) ? (1u << 20) : (bytes > kMaxSpan ? kMaxSpan : bytes);
+  return g_chunk_bytes.exchange(b, std::memory_order_relaxed);
+}
 
 }  // extern "C"

@@ -644,10 +644,25 @@ def test_host_resident_pipeline(dev, oracle):
     assert np.nonzero(mm)[0].tolist() == [12345]
 
 
-def test_host_pipeline_mixed_large_spans(dev, oracle):
-    """Host batches whose spans straddle the 32 MiB DMA chunk size: small
-    spans, a 48 MiB span (its own chunk), a 64 MiB - 4 span verified with its
-    trailer, then small spans again; with per-span init."""
+@pytest.fixture(params=[32, 64])
+def pipe_chunk(request):
+    """The host pipeline's chunk size (tuning hook; 64 MiB by default)."""
+    import ctypes
+
+    from prismdb_amd import _lib
+
+    L = _lib.lib()
+    L.prismdb_pipeline_chunk_bytes.restype = ctypes.c_size_t
+    L.prismdb_pipeline_chunk_bytes.argtypes = [ctypes.c_size_t]
+    prev = L.prismdb_pipeline_chunk_bytes(request.param << 20)
+    yield request.param
+    L.prismdb_pipeline_chunk_bytes(prev)
+
+
+def test_host_pipeline_mixed_large_spans(dev, oracle, pipe_chunk):
+    """Host batches whose spans straddle the DMA chunk size (32 and 64 MiB):
+    small spans, a 48 MiB span, a 64 MiB - 4 span verified with its trailer,
+    then small spans again; with per-span init."""
     from prismdb_amd import crc32c
 
     lens = [3988] * 300 + [48 << 20, 1000, (64 << 20) - 4] + [4096] * 300 + [7, 0, 1]
@@ -671,7 +686,22 @@ def test_host_pipeline_mixed_large_spans(dev, oracle):
     assert np.nonzero(mm)[0].tolist() == [302]
 
 
-def test_host_pipeline_failure_drains_ring(dev, oracle):
+@pytest.fixture
+def pipe_chunk32():
+    """32 MiB host pipeline chunks for the test (the default is 64 MiB)."""
+    import ctypes
+
+    from prismdb_amd import _lib
+
+    L = _lib.lib()
+    L.prismdb_pipeline_chunk_bytes.restype = ctypes.c_size_t
+    L.prismdb_pipeline_chunk_bytes.argtypes = [ctypes.c_size_t]
+    prev = L.prismdb_pipeline_chunk_bytes(32 << 20)
+    yield 32
+    L.prismdb_pipeline_chunk_bytes(prev)
+
+
+def test_host_pipeline_failure_drains_ring(dev, oracle, pipe_chunk32):
     """A host batch that fails after several chunks are in flight returns its
     ring to the pool empty: the next, smaller call (which leases it again)
     gets its own results only and nothing is written past its output arrays."""
@@ -681,7 +711,7 @@ def test_host_pipeline_failure_drains_ring(dev, oracle):
 
     L = _lib.lib()
     L.prismdb_pipeline_fail_after.argtypes = [ctypes.c_int]
-    n = 40000  # ~152 MiB at stride 3992: five 32 MiB chunks
+    n = 40000  # ~152 MiB at stride 3992: five 32 MiB chunks (pipe_chunk32), three in flight at the failure
     off = np.arange(n, dtype=np.uint64) * 3992
     lens = np.full(n, 3988, dtype=np.uint32)
     host = oracle.synth(n * 3992 + 8, 0x5EED0010)
