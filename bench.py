@@ -35,8 +35,11 @@ Printed (rank 0): ONE JSON line with the driver's contract fields plus
                 leveldb_crc32c_batch_multi over all N devices: PrismDB's shape,
                 8 partition threads of one process (db/db_impl.h:359,
                 util/env_posix.cc:850-890); one RCCL clique of N devices
-                (ncclCommInitAll), results gathered to device 0 over xGMI
-                (--no-multi skips it)
+                (ncclCommInitAll), results gathered to device 0 over xGMI;
+                per device its batch and gather times (HIP events on the
+                clique streams) and the clique's ncclCommInitAll wall time
+                (--no-multi skips it; at N = 1, --multi-devices picks the
+                device count, default 1)
 """
 from __future__ import annotations
 
@@ -52,6 +55,9 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+# config5_leg times windows next to the planner path with the library's
+# prismdb_crc32c_windows setter, which acts only with this set
+os.environ.setdefault("PRISMDB_ENABLE_TEST_HOOKS", "1")
 
 METRIC = "GiB/s CRC32C over device-resident 4 KiB SST blocks; bit-exact vs util/crc32c.cc"
 SEED = 0x5EED0001
@@ -82,7 +88,8 @@ def parse():
     ap.add_argument("--multi-timeout", type=float, default=240.0,
                     help="seconds the batch_multi leg's child process may take before it is stopped")
     ap.add_argument("--multi-child", action="store_true", help=argparse.SUPPRESS)
-    ap.add_argument("--multi-devices", type=int, default=0, help=argparse.SUPPRESS)
+    ap.add_argument("--multi-devices", type=int, default=0,
+                    help="at --gpus 1: devices of the one-process batch_multi leg (default 1)")
     ap.add_argument("--cpu-all-blocks", type=int, default=1 << 20,
                     help="cpu_baseline all-cores figure: blocks (config 1: 1 Mi x 4 KiB)")
     return ap.parse_args()
@@ -100,6 +107,60 @@ def cpu_threads() -> int:
     if env and env.isdigit():
         n = min(n, int(env))
     return max(1, n)
+
+
+def cpu_quota():
+    """CPUs the process's cgroup lets it use (CFS quota / period, rounded up;
+    the tightest level of its hierarchy), or None without a quota.  cgroup v2
+    (cpu.max) and v1 (cpu.cfs_quota_us / cpu.cfs_period_us)."""
+    best = None
+    try:
+        with open("/proc/self/cgroup") as f:
+            lines = [ln.strip().split(":", 2) for ln in f if ln.strip()]
+    except OSError:
+        return None
+    for _, ctrl, path in lines:
+        if ctrl == "":
+            base, files = "/sys/fs/cgroup", ("cpu.max",)
+        elif "cpu" in ctrl.split(","):
+            base, files = "/sys/fs/cgroup/cpu", ("cpu.cfs_quota_us", "cpu.cfs_period_us")
+        else:
+            continue
+        parts = [p for p in path.split("/") if p]
+        for k in range(len(parts), -1, -1):  # the cgroup and each ancestor
+            d = os.path.join(base, *parts[:k])
+            try:
+                if len(files) == 1:
+                    with open(os.path.join(d, files[0])) as f:
+                        q, per = f.read().split()[:2]
+                else:
+                    with open(os.path.join(d, files[0])) as f:
+                        q = f.read().strip()
+                    with open(os.path.join(d, files[1])) as f:
+                        per = f.read().strip()
+            except (OSError, ValueError):
+                continue
+            if q in ("max", "-1") or int(per) <= 0:
+                continue
+            n = max(1, -(-int(q) // int(per)))
+            best = n if best is None else min(best, n)
+    return best
+
+
+def all_core_threads():
+    """Threads for the config-1 "all host cores" figure: the CPUs the process
+    may actually use -- its affinity set, bounded by its cgroup CPU quota, else
+    by OMP_NUM_THREADS (the box's CPU share for one GPU).  Threads beyond the
+    quota only time-slice: round 4 ran 256 threads on a 16-CPU share and
+    measured 47.8 GiB/s against 220.4 on 16."""
+    n = len(affinity())
+    q = cpu_quota()
+    if q is not None:
+        return min(n, q), f"cgroup CPU quota {q}, affinity {n}"
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit():
+        return min(n, int(env)), f"no cgroup quota; OMP_NUM_THREADS {env}, affinity {n}"
+    return n, f"no cgroup quota; affinity {n}"
 
 
 def _ranges(cpus: list) -> str:
@@ -195,22 +256,24 @@ def cpu_baseline_leg(args, gpu_out, dev_buf) -> dict | None:
         "cpu_model": cpu_model(),
         "agrees_with_gpu": f"{agree}/{nblk}",
     }
-    # config 1 as SURVEY 8(d) states it: 1 Mi x 4 KiB at all host cores (the
-    # affinity set), bytes from the device buffer (the same stream)
+    # config 1 as SURVEY 8(d) states it: 1 Mi x 4 KiB at all host cores --
+    # the CPUs this process may use (all_core_threads), bytes from the device
+    # buffer (the same stream)
     nall = min(args.cpu_all_blocks, args.nblocks)
     if kind == "reference" and nall > 0:
         big = dev_buf[:nall * BLOCK].cpu().numpy()
         oall = np.empty(nall, dtype=np.uint32)
-        nthr = len(cpus)
-        t_one = max(run(nthr, 1, big, oall, nall), 1e-6)  # one calibration pass: the box may give this
-        p_all = max(1, min(64, int(round(2.0 / t_one))))  # process fewer cores than its affinity set; ~2 s
+        nthr, why = all_core_threads()
+        t_one = max(run(nthr, 1, big, oall, nall), 1e-6)  # one calibration pass
+        p_all = max(1, min(64, int(round(2.0 / t_one))))  # ~2 s
         ta = run(nthr, p_all, big, oall, nall)
         ga = gpu_out[:nall].cpu().numpy().view(np.uint32)
         res["all_cores"] = {
             "value": round(nall * BLOCK * p_all / ta / GIB, 3), "unit": "GiB/s", "threads": nthr,
+            "threads_from": why,
             "blocks": nall, "passes": p_all, "wall_s": round(ta, 3),
-            "sample": f"config 1: crc32c::Value over {nall} x 4096 B host-resident blocks on every core of the "
-                      f"affinity set ({nthr} threads; the box's CPU share for one GPU may be smaller)",
+            "sample": f"config 1: crc32c::Value over {nall} x 4096 B host-resident blocks on all {nthr} CPUs "
+                      f"this process may use ({why})",
             "agrees_with_gpu": f"{int((ga == oall).sum())}/{nall}",
         }
         del big
@@ -289,7 +352,8 @@ def compaction_leg(torch, crc32c, dev, nfiles: int = 115) -> dict:
       read  (input SSTs)  ReadBlock verify of every block: Unmask(stored) ==
                           Value(contents||type)  (table/format.cc:93-101)
       write (output SSTs) WriteRawBlock's Mask(Value(contents||type)) for every
-                          block, stored into the 5-byte trailers by the host
+                          block, stored into the 5-byte trailers by the engine
+                          (batch_host with WRITE_TRAILER)
     Both through leveldb_crc32c_batch_host; GiB/s of block bytes incl. all
     copies.  Never the headline value."""
     import numpy as np
@@ -324,23 +388,18 @@ def compaction_leg(torch, crc32c, dev, nfiles: int = 115) -> dict:
         clean = clean and int(mm.sum()) == 0
     res["read_verify"] = round(best, 2)
     res["read_all_blocks_verified"] = clean
-    img[tr] = 0
-    # the trailer slots as strided views (per file: the data blocks' at stride
-    # 3992, then the index block's), so that the host's own stores -- what
-    # TableBuilder does after each block -- are plain strided copies
-    files = img.reshape(nfiles, file_bytes)
-    data_tr = files[:, :ndata * stride].reshape(nfiles, ndata, stride)[:, :, data_n + 1:data_n + 5]
-    index_tr = files[:, ndata * stride + index_n + 1:ndata * stride + index_n + 5]
-    best = 0.0
+    # the engine stores each block's trailer into the host image as it seals
+    # (WRITE_TRAILER: 4 LE bytes behind each block, table/table_builder.cc:192-197),
+    # chunk by chunk while the next chunks are in flight
+    best, exact = 0.0, True
     for _ in range(3):
+        img[tr] = 0
         t0 = time.perf_counter()
-        crc, _ = crc32c.batch_host(img, off, lens, mask=True)
-        c = crc.astype("<u4").view(np.uint8).reshape(nfiles, ndata + 1, 4)
-        data_tr[:] = c[:, :ndata]
-        index_tr[:] = c[:, ndata]
+        crc32c.batch_host(img, off, lens, mask=True, trailer=True)
         best = max(best, nbytes / (time.perf_counter() - t0) / GIB)
+        exact = exact and bool((img[tr] == want).all())
     res["write_seal"] = round(best, 2)
-    res["write_trailers_match_reference_layout"] = bool((img[tr] == want).all())
+    res["write_trailers_match_reference_layout"] = exact
     res["unit"] = "GiB/s"
     return res
 
@@ -552,6 +611,16 @@ def multi_leg(args, torch, crc32c, ndev: int) -> dict:
         el = time.perf_counter() - t0
         res[name] = {"value": round(ndev * nfiles * span_bytes * args.c5_steps / el / GIB, 2), "unit": "GiB/s",
                      "ms_per_step": round(el * 1e3 / args.c5_steps, 3)}
+        if name == "with_gather":
+            # the last step's phases on each device (HIP events on the clique
+            # streams) and the clique's one-time ncclCommInitAll
+            tm = crc32c.multi_timing(list(range(ndev)))
+            if tm is not None:
+                res["init_ms_ncclCommInitAll"] = tm["init_ms"]
+                res[name]["per_device_batch_ms"] = tm["batch_ms"]
+                res[name]["per_device_gather_ms"] = tm["gather_ms"]
+                res[name]["per_device_GiB_s"] = [round(nfiles * span_bytes / (b / 1e3) / GIB, 1) if b > 0 else None
+                                                 for b in tm["batch_ms"]]
     want = torch.cat([t.to(root) for t in sep])
     res["gather_check"] = {"gathered_equals_per_device": bool(torch.equal(out, want)), "entries": int(out.numel())}
     crc32c.batch_multi(parts, verify=True, out=out, mismatch=mm, streams=streams, check_bounds=False)
@@ -738,14 +807,16 @@ def main() -> int:
     multi = None
     if not args.no_multi:
         # one child process of rank 0 drives the devices (all `world` ranks'
-        # devices; at world 1 every visible device, PrismDB's one-process
-        # shape); the ranks free their memory and wait on the host
+        # devices: PrismDB's one-process shape); the ranks free their memory
+        # and wait on the host
         del outs
         torch.cuda.empty_cache()
         if world > 1:
             dist.barrier(group=cpu_group)
         if rank == 0:
-            ndev = world if world > 1 else max(1, min(8, torch.cuda.device_count()))
+            # the ranks' devices; at world 1 --multi-devices (default: the
+            # one device the caller asked for, not every visible one)
+            ndev = world if world > 1 else max(1, args.multi_devices or 1)
             multi = run_multi_child(args, ndev)
         if world > 1:
             dist.barrier(group=cpu_group)

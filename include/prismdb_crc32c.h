@@ -100,6 +100,11 @@ int leveldb_crc32c_batch_fixed(const void* dev_base, size_t stride, size_t len, 
  * Variable batch: block i = base[off[i], off[i] + len[i]); init[i] per block
  * (dev_init may be NULL: all 0).  Any byte alignment, any length (< 4 GiB).
  * Long spans are split across many wavefronts and recombined on the device.
+ * Routing is by span count alone: <= 2^17 spans one kernel launch (an SST
+ * file, a log file); 2^17 < n <= 2^18 spans without LOG_HEADER two such
+ * launches (a compaction's dozen files: uniform SST blocks run faster that
+ * way, batches of very mixed span sizes ~10 points of roofline slower than on
+ * the planner path); beyond, the planner path (task-balanced slices).
  */
 int leveldb_crc32c_batch(const void* dev_base, const uint64_t* dev_off, const uint32_t* dev_len,
                          const uint32_t* dev_init, size_t n, uint32_t* dev_out,
@@ -114,8 +119,14 @@ int leveldb_crc32c_batch(const void* dev_base, const uint64_t* dev_off, const ui
  * -> batch kernel -> results back, four chunks in flight on the engine's own
  * streams.  Synchronous; out/mismatch are host arrays (either may be NULL).
  * flags: PRISMDB_CRC32C_MASK, PRISMDB_CRC32C_LOG_HEADER (verify log records:
- * the 6 header bytes before each span travel with it).  Uses the current HIP
- * device.
+ * the 6 header bytes before each span travel with it), and
+ * PRISMDB_CRC32C_WRITE_TRAILER (not with mismatch): each span's (masked)
+ * result is stored into host_base as its trailer -- 4 LE bytes right after
+ * the span, or with LOG_HEADER the header crc 6 bytes before it -- as
+ * TableBuilder::WriteRawBlock appends it (table/table_builder.cc:192-197); the
+ * buffer must then be writable and no trailer may overlap a span of the batch.
+ * On an error return, the trailers of chunks already finished may be written.
+ * Uses the current HIP device.
  */
 int leveldb_crc32c_batch_host(const void* host_base, const uint64_t* off, const uint32_t* len,
                               const uint32_t* init, size_t n, uint32_t* out, uint8_t* mismatch,

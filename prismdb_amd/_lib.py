@@ -65,7 +65,8 @@ def _declare(lib: ctypes.CDLL) -> None:
         "leveldb_crc32c_last_error": (ctypes.c_char_p, []),
         "prismdb_fill_synthetic": (ctypes.c_int, [vp, sz, u64, u64, vp]),
         "prismdb_crc32c_extend_portable": (u32, [u32, cp, sz]),
-        # test hooks (not in the public headers): path pinning
+        # test hooks (not in the public headers): path pinning -- the setters
+        # act only with PRISMDB_ENABLE_TEST_HOOKS=1 in the environment
         "prismdb_crc32c_force_generic": (None, [ctypes.c_int]),
         "prismdb_crc32c_lane_mode": (None, [ctypes.c_int]),
         "prismdb_crc32c_direct_max": (u64, [u64]),
@@ -78,6 +79,8 @@ def _declare(lib: ctypes.CDLL) -> None:
         "prismdb_crc32c_direct_set_gen": (ctypes.c_int, [vp, u32]),
         "prismdb_crc32c_multi_fail_after": (ctypes.c_int, [ctypes.c_int]),
         "prismdb_crc32c_windows": (ctypes.c_int, [ctypes.c_int]),
+        "prismdb_crc32c_multi_timing": (ctypes.c_int, [ctypes.c_int, vp, vp, vp, vp]),
+        "prismdb_test_hooks_enabled": (ctypes.c_int, []),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

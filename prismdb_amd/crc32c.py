@@ -256,11 +256,34 @@ def batch_multi(parts, *, mask: bool = False, verify: bool = False, trailer: boo
     return out, (mismatch if verify else None)
 
 
-def batch_host(base, off, lens, init=None, *, mask: bool = False, verify: bool = False, log_header: bool = False):
+def multi_timing(devices):
+    """Phases of the last batch_multi call on this device list (diagnostics,
+    HIP events on the clique's streams): {"batch_ms": [per device],
+    "gather_ms": [per device], "init_ms": ncclCommInitAll's wall time}, or
+    None if there was no such call."""
+    ndev = len(devices)
+    c_dev = (ctypes.c_int * ndev)(*devices)
+    b, g = (ctypes.c_float * ndev)(), (ctypes.c_float * ndev)()
+    init = ctypes.c_double(0)
+    rc = lib().prismdb_crc32c_multi_timing(ndev, c_dev, b, g, ctypes.byref(init))
+    if rc != 0:
+        return None
+    return {"batch_ms": [round(x, 3) for x in b], "gather_ms": [round(x, 3) for x in g],
+            "init_ms": round(init.value, 1)}
+
+
+def batch_host(base, off, lens, init=None, *, mask: bool = False, verify: bool = False, log_header: bool = False,
+               trailer: bool = False):
     """Host-resident batch: numpy (or pinned torch CPU tensor) buffer and
     descriptors in host memory; streamed through the device by the engine.
+    trailer=True stores each (masked, with mask=True) result into `base` as
+    the span's trailer (4 LE bytes after it; with log_header, the record
+    header's crc 6 bytes before it), as TableBuilder::WriteRawBlock does.
     Returns (crc uint32[n], mismatch uint8[n] or None) as numpy arrays."""
     import numpy as np
+
+    if trailer and verify:
+        raise ValueError("trailer and verify are exclusive")
 
     n = len(off)
     off = np.asarray(off)
@@ -273,7 +296,7 @@ def batch_host(base, off, lens, init=None, *, mask: bool = False, verify: bool =
         raise ValueError("off, lens and init must have the same length")
     nbytes = base.numel() * base.element_size() if hasattr(base, "data_ptr") else base.nbytes
     if n:
-        lead, tail = _span_reach(log_header, verify, False)
+        lead, tail = _span_reach(log_header, verify, trailer)
         lo, omax = int(off.min()), int(off.max())
         # 0 <= off <= nbytes for every span first: then no off + len wraps
         hi = int((off + lens.astype(np.uint64)).max()) if omax <= nbytes else omax
@@ -285,7 +308,8 @@ def batch_host(base, off, lens, init=None, *, mask: bool = False, verify: bool =
     rc = lib().leveldb_crc32c_batch_host(ptr, off.ctypes.data, lens.ctypes.data,
                                          ini.ctypes.data if ini is not None else None, n, out.ctypes.data,
                                          mm.ctypes.data if verify else None,
-                                         (FLAG_MASK if mask else 0) | (FLAG_LOG_HEADER if log_header else 0))
+                                         (FLAG_MASK if mask else 0) | (FLAG_LOG_HEADER if log_header else 0)
+                                         | (FLAG_WRITE_TRAILER if trailer else 0))
     check(rc, "leveldb_crc32c_batch_host")
     return out, mm
 

@@ -13,6 +13,7 @@
 
 #include <atomic>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <list>
 #include <mutex>
@@ -45,6 +46,18 @@ thread_local hipStream_t t_last_stream = nullptr;
 thread_local bool t_last_direct = false;
 thread_local bool t_last_pair = false;  // the planner batch launched the pair-run kernel
 thread_local const uint32_t* t_last_stats = nullptr;
+// Whether that batch ran on an engine-owned stream (a pipeline ring, a clique
+// stream), whose workspace any thread may release (ReleaseEngineStream), and
+// the release epoch then: the hooks above refuse to read it after a release.
+thread_local bool t_last_owned = false;
+thread_local uint64_t t_last_epoch = 0;
+std::atomic<uint64_t> g_release_epoch{0};
+
+// The calling thread's last batch ran on an engine stream whose workspace
+// has been released since (by any thread): its pointers are gone.
+bool LastBatchStale() {
+  return t_last_owned && t_last_epoch != g_release_epoch.load(std::memory_order_acquire);
+}
 
 int Fail(int code, const std::string& msg) {
   t_last_error = msg;
@@ -262,6 +275,7 @@ struct Workspace {
   size_t cap_q = 0;
   char* direct = nullptr;  // word, done | ticket map | partials | per-span counters
   uint32_t gen = 0;
+  bool owned = false;  // an engine stream's (g_owned), not a thread's
   SplitWs ws{};
 };
 
@@ -330,7 +344,14 @@ WorkspaceCache& ThreadWorkspaces() {
 // cycled through the LRU.
 std::mutex g_owned_mu;
 std::list<Workspace> g_owned;  // (list: entries never move)
-std::atomic<int> g_owned_count{0};
+// Lock-free snapshot of the owned streams' handles, so a batch on any other
+// stream -- every PrismDB partition thread's own -- never takes g_owned_mu:
+// slots are written under the mutex, read with relaxed loads.  More engine
+// streams than slots at once (not reached: kKeepIdle rings per device plus
+// the live leases and clique streams) send every lookup through the mutex.
+constexpr int kOwnedSlots = 256;
+std::atomic<hipStream_t> g_owned_keys[kOwnedSlots];
+std::atomic<int> g_owned_spill{0};  // registered streams that found no free slot
 
 // Allocates w's fixed part on stream s (device current).
 int InitWorkspace(Workspace& w, int device, hipStream_t s) {
@@ -375,7 +396,10 @@ Workspace* FindWorkspace(hipStream_t s, int& rc) {
     rc = FailHip(e, "hipGetDevice");
     return nullptr;
   }
-  if (g_owned_count.load(std::memory_order_acquire) > 0) {
+  bool maybe_owned = s != nullptr && g_owned_spill.load(std::memory_order_acquire) > 0;
+  for (int k = 0; k < kOwnedSlots && !maybe_owned && s != nullptr; ++k)
+    maybe_owned = g_owned_keys[k].load(std::memory_order_acquire) == s;
+  if (maybe_owned) {
     std::lock_guard<std::mutex> lk(g_owned_mu);
     for (Workspace& w : g_owned) {
       if (w.stream != s) continue;
@@ -383,6 +407,7 @@ Workspace* FindWorkspace(hipStream_t s, int& rc) {
         w.stream = s;  // (stays registered: the next call retries)
         return nullptr;
       }
+      w.owned = true;
       rc = 0;
       return &w;
     }
@@ -581,6 +606,8 @@ int RunBatch(DeviceCtx& ctx, const SpanBatch& base_args, bool desc, bool verify,
     t_last_direct = true;
     t_last_stats = d.stats;
     t_last_stream = s;
+    t_last_owned = w->owned;
+    t_last_epoch = g_release_epoch.load(std::memory_order_acquire);
     mark.by_launch = true;
     hipError_t e = prismdb::dev::launch_direct(a, verify, ctx.cus, d, s, w->done[w->gen & 1u]);
     return e == hipSuccess ? 0 : FailHip(e, "direct kernel launch");
@@ -617,7 +644,7 @@ int RunBatch(DeviceCtx& ctx, const SpanBatch& base_args, bool desc, bool verify,
   // The span kernel's record streams: two per wave of its persistent grid.
   // (Round 4 tried one task sequence per wave here, the one-launch kernel's
   // ring: within +-2 % on the bulk rows, profiles/r04/r04i_configs_*.json;
-  // its sources are tools/patches/span1/.)
+  // its kernels are in git history: crc32c_kernels.hip at 36498f1.)
   const uint32_t streams = 2u * (uint32_t)ctx.cus * prismdb::dev::kWavesPerGroup;
   if ((rc = PlannerWorkspace(*w, s, a.n, streams, lane, &ws)) != 0) return rc;
   hipError_t e = hipMemsetAsync(ws.counters, 0, sizeof(SplitCounters), s);
@@ -625,6 +652,8 @@ int RunBatch(DeviceCtx& ctx, const SpanBatch& base_args, bool desc, bool verify,
   t_last_counters = ws.counters;
   t_last_stream = s;
   t_last_direct = false;
+  t_last_owned = w->owned;
+  t_last_epoch = g_release_epoch.load(std::memory_order_acquire);
   uint32_t* const caller_out = a.out;
   uint8_t* const caller_mm = a.mismatch;
   if (lane) {
@@ -691,6 +720,21 @@ int RunBatch(DeviceCtx& ctx, const SpanBatch& base_args, bool desc, bool verify,
 namespace prismdb {
 void SetLastError(const std::string& msg) { t_last_error = msg; }
 
+// The prismdb_* setters below (and the pipeline's and batch_multi's) change
+// process-global routing or inject failures: one PrismDB partition thread
+// calling one would reroute or fail every other thread's batches.  They act
+// only when the process runs with PRISMDB_ENABLE_TEST_HOOKS=1 (read at the
+// first hook call; the tests, the bench and the tools set it); otherwise
+// each is a no-op that reports the current setting and sets the last error.
+bool TestHooksEnabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("PRISMDB_ENABLE_TEST_HOOKS");
+    return e != nullptr && e[0] == '1' && e[1] == '\0';
+  }();
+  if (!on) t_last_error = "test hooks are off (set PRISMDB_ENABLE_TEST_HOOKS=1)";
+  return on;
+}
+
 // The engine's own streams (pipeline rings, clique streams): one workspace
 // per stream, whichever thread calls on it (one at
 // a time: a leased ring, the owning workspace's thread, the clique's mutex);
@@ -700,7 +744,13 @@ void RegisterEngineStream(hipStream_t s) {
   std::lock_guard<std::mutex> lk(g_owned_mu);
   g_owned.emplace_back();
   g_owned.back().stream = s;
-  g_owned_count.fetch_add(1, std::memory_order_release);
+  for (int k = 0; k < kOwnedSlots; ++k) {
+    if (g_owned_keys[k].load(std::memory_order_relaxed) == nullptr) {
+      g_owned_keys[k].store(s, std::memory_order_release);
+      return;
+    }
+  }
+  g_owned_spill.fetch_add(1, std::memory_order_release);
 }
 
 void ReleaseEngineStream(hipStream_t s) {
@@ -710,11 +760,21 @@ void ReleaseEngineStream(hipStream_t s) {
     for (auto it = g_owned.begin(); it != g_owned.end(); ++it) {
       if (it->stream == s) {
         gone.splice(gone.begin(), g_owned, it);
-        g_owned_count.fetch_sub(1, std::memory_order_release);
+        bool slot = false;
+        for (int k = 0; k < kOwnedSlots && !slot; ++k) {
+          if (g_owned_keys[k].load(std::memory_order_relaxed) == s) {
+            g_owned_keys[k].store(nullptr, std::memory_order_release);
+            slot = true;
+          }
+        }
+        if (!slot) g_owned_spill.fetch_sub(1, std::memory_order_release);
         break;
       }
     }
   }
+  // Other threads' last-batch pointers into this workspace go stale: the
+  // epoch tells their hooks so.
+  g_release_epoch.fetch_add(1, std::memory_order_acq_rel);
   for (Workspace& w : gone)
     if (w.mem != nullptr) SyncAndRelease(w);
 }
@@ -790,14 +850,21 @@ int leveldb_crc32c_batch(const void* dev_base, const uint64_t* dev_off, const ui
 
 const char* leveldb_crc32c_last_error(void) { return t_last_error.c_str(); }
 
+// 1 if the prismdb_* test and tuning setters act in this process
+// (PRISMDB_ENABLE_TEST_HOOKS=1), else 0.
+int prismdb_test_hooks_enabled(void) { return prismdb::TestHooksEnabled() ? 1 : 0; }
+
 // Test hooks, not in the public header (the parity tests and the A/B harness
-// pin each path with them):
+// pin each path with them; no-ops unless PRISMDB_ENABLE_TEST_HOOKS=1):
 // fixed-stride batches through the generic span kernel too;
-void prismdb_crc32c_force_generic(int on) { g_force_generic.store(on != 0, std::memory_order_relaxed); }
+void prismdb_crc32c_force_generic(int on) {
+  if (prismdb::TestHooksEnabled()) g_force_generic.store(on != 0, std::memory_order_relaxed);
+}
 
 // which planner-path descriptor batches take the lane kernel first (0 =
 // log-record batches, the default; 1 = every batch; -1 = none);
 void prismdb_crc32c_lane_mode(int mode) {
+  if (!prismdb::TestHooksEnabled()) return;
   g_lane_mode.store(mode > 0 ? 1 : (mode < 0 ? -1 : 0), std::memory_order_relaxed);
 }
 
@@ -805,6 +872,7 @@ void prismdb_crc32c_lane_mode(int mode) {
 // (clamped to kDirectMaxSpans; 0: none do; larger batches: windows of this
 // many spans, see prismdb_crc32c_windows); returns the previous value.
 uint64_t prismdb_crc32c_direct_max(uint64_t n) {
+  if (!prismdb::TestHooksEnabled()) return g_direct_max.load(std::memory_order_relaxed);
   if (n > prismdb::dev::kDirectMaxSpans) n = prismdb::dev::kDirectMaxSpans;
   return g_direct_max.exchange(n, std::memory_order_relaxed);
 }
@@ -812,17 +880,22 @@ uint64_t prismdb_crc32c_direct_max(uint64_t n) {
 // the one-launch path's ticket capacity (clamped to 1..kDirectTickets) and
 // debug flags (bit 0: delay the pushes, see DirectWs::dbg); return the old values.
 uint32_t prismdb_crc32c_direct_tickets(uint32_t cap) {
+  if (!prismdb::TestHooksEnabled()) return g_direct_cap.load(std::memory_order_relaxed);
   if (cap < 1u) cap = 1u;
   if (cap > prismdb::dev::kDirectTickets) cap = prismdb::dev::kDirectTickets;
   return g_direct_cap.exchange(cap, std::memory_order_relaxed);
 }
-uint32_t prismdb_crc32c_direct_debug(uint32_t flags) { return g_direct_dbg.exchange(flags, std::memory_order_relaxed); }
+uint32_t prismdb_crc32c_direct_debug(uint32_t flags) {
+  if (!prismdb::TestHooksEnabled()) return g_direct_dbg.load(std::memory_order_relaxed);
+  return g_direct_dbg.exchange(flags, std::memory_order_relaxed);
+}
 
 // descriptor batches of more than prismdb_crc32c_direct_max spans (log-record
 // batches aside): 1 = windows of the one-launch kernel, 0 = the planner path,
 // 2 = windows up to two of them, the planner beyond (default); returns the
 // previous value.
 int prismdb_crc32c_windows(int mode) {
+  if (!prismdb::TestHooksEnabled()) return g_windows.load(std::memory_order_relaxed);
   return g_windows.exchange(mode < 0 || mode > 2 ? 2 : mode, std::memory_order_relaxed);
 }
 
@@ -831,6 +904,7 @@ int prismdb_crc32c_windows(int mode) {
 // bits; gen + 1 == 0 mod 2^16 zeroes the workspace first).  Lets a test cross
 // the tag wrap in a few calls.  0, or -1 if the thread has no such workspace.
 int prismdb_crc32c_direct_set_gen(void* stream, uint32_t gen) {
+  if (!prismdb::TestHooksEnabled()) return -1;
   int device = 0;
   if (hipGetDevice(&device) != hipSuccess) return -1;
   for (Workspace& w : ThreadWorkspaces().lru) {
@@ -846,7 +920,7 @@ int prismdb_crc32c_direct_set_gen(void* stream, uint32_t gen) {
 // last one-launch batch {tickets adopted, spans folded whole, tickets claimed
 // early, tickets claimed late}, after waiting for its stream.  0, or -1.
 int prismdb_crc32c_direct_stats(uint64_t out[4]) {
-  if (t_last_stats == nullptr) return -1;
+  if (t_last_stats == nullptr || LastBatchStale()) return -1;
   uint32_t c[4] = {0, 0, 0, 0};
   hipError_t e = hipStreamSynchronize(t_last_stream);
   if (e == hipSuccess) e = hipMemcpy(c, t_last_stats, sizeof(c), hipMemcpyDeviceToHost);
@@ -861,7 +935,7 @@ int prismdb_crc32c_direct_stats(uint64_t out[4]) {
 // no such batch; -2 if its last descriptor batch took the one-launch path.
 int prismdb_crc32c_last_split(uint64_t out[4]) {
   if (t_last_direct) return -2;
-  if (t_last_counters == nullptr) return -1;
+  if (t_last_counters == nullptr || LastBatchStale()) return -1;
   prismdb::dev::SplitCounters c{};
   hipError_t e = hipStreamSynchronize(t_last_stream);
   if (e == hipSuccess) e = hipMemcpy(&c, t_last_counters, sizeof(c), hipMemcpyDeviceToHost);
@@ -880,7 +954,7 @@ int prismdb_crc32c_last_split(uint64_t out[4]) {
 // batch, -1 before any planner batch.
 int prismdb_crc32c_last_schedule(uint64_t out[3]) {
   if (t_last_direct) return -2;
-  if (t_last_counters == nullptr) return -1;
+  if (t_last_counters == nullptr || LastBatchStale()) return -1;
   prismdb::dev::SplitCounters c{};
   hipError_t e = hipStreamSynchronize(t_last_stream);
   if (e == hipSuccess) e = hipMemcpy(&c, t_last_counters, sizeof(c), hipMemcpyDeviceToHost);

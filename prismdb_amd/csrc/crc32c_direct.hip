@@ -346,7 +346,8 @@ __global__ __launch_bounds__(kDirectThreads) void crc32c_direct_kernel(SpanBatch
   }
 
   // The claim word of the call after next starts at zero (calls take four
-  // words in turn, and at most two calls of a stream run at once).
+  // words in turn and a stream's calls run in order -- every launch is
+  // ordered -- so that word is idle).
   if (wave == 0 && lane == 0) __hip_atomic_store(d.next, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 
   {

@@ -19,6 +19,7 @@
 #include <rccl/rccl.h>
 
 #include <atomic>
+#include <chrono>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -30,6 +31,7 @@
 namespace prismdb {
 void SetLastError(const std::string& msg);  // crc32c_capi.hip: leveldb_crc32c_last_error()
 void RegisterEngineStream(hipStream_t s);   // crc32c_capi.hip: the stream's own batch workspace
+bool TestHooksEnabled();                    // crc32c_capi.hip: PRISMDB_ENABLE_TEST_HOOKS
 }
 
 namespace {
@@ -55,6 +57,12 @@ struct Clique {
   std::vector<uint32_t*> out;        // per device (index 0 unused): its partition's results
   std::vector<uint8_t*> mm;
   std::vector<size_t> cap;
+  // Per device, timing events of the last call on the clique stream: after
+  // the hand-off from the caller (t0), after the device's own batch (t1),
+  // after the gather (t2) -- read back by prismdb_crc32c_multi_timing.
+  std::vector<hipEvent_t> t0, t1, t2;
+  bool timed = false;  // the last call recorded all three
+  double init_ms = 0;  // ncclCommInitAll's wall time
   std::mutex mu;
 };
 
@@ -75,8 +83,10 @@ int GetClique(int ndev, const int* devices, Clique** out) {
   std::unique_ptr<Clique> c(new Clique);
   c->devs.assign(devices, devices + ndev);
   c->comms.resize(ndev);
+  const auto w0 = std::chrono::steady_clock::now();
   ncclResult_t r = ncclCommInitAll(c->comms.data(), ndev, devices);
   if (r != ncclSuccess) return NcclFail(r, "ncclCommInitAll");
+  c->init_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - w0).count();
   int cur = 0;
   (void)hipGetDevice(&cur);
   c->streams.resize(ndev);
@@ -84,11 +94,17 @@ int GetClique(int ndev, const int* devices, Clique** out) {
   c->out.assign(ndev, nullptr);
   c->mm.assign(ndev, nullptr);
   c->cap.assign(ndev, 0);
+  c->t0.assign(ndev, nullptr);
+  c->t1.assign(ndev, nullptr);
+  c->t2.assign(ndev, nullptr);
   for (int p = 0; p < ndev; ++p) {
     hipError_t e = hipSetDevice(devices[p]);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->streams[p], hipStreamNonBlocking);
     if (e == hipSuccess) prismdb::RegisterEngineStream(c->streams[p]);  // (used under the clique's mutex)
     if (e == hipSuccess) e = hipEventCreateWithFlags(&c->events[p], hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreate(&c->t0[p]);
+    if (e == hipSuccess) e = hipEventCreate(&c->t1[p]);
+    if (e == hipSuccess) e = hipEventCreate(&c->t2[p]);
     if (e != hipSuccess) {
       (void)hipSetDevice(cur);
       return HipFail(e, "clique streams");
@@ -137,6 +153,7 @@ int leveldb_crc32c_batch_multi(int ndev, const int* devices, const void* const* 
   int rc = GetClique(ndev, devices, &c);
   if (rc != 0) return rc;
   std::lock_guard<std::mutex> lk(c->mu);
+  c->timed = false;
   // Once the first command is on a clique stream, every return goes through
   // here: the caller's streams wait for everything the call enqueued (its
   // batches, scratch growth, the gather), so a caller that frees or reuses
@@ -166,6 +183,7 @@ int leveldb_crc32c_batch_multi(int ndev, const int* devices, const void* const* 
     if ((e = hipStreamWaitEvent(c->streams[p], c->events[p], 0)) != hipSuccess)
       return finish(HipFail(e, "hipStreamWaitEvent"));
     enqueued = p + 1;
+    if ((e = hipEventRecord(c->t0[p], c->streams[p])) != hipSuccess) return finish(HipFail(e, "hipEventRecord"));
     if (p > 0 && c->cap[p] < n[p]) {
       if (c->out[p] != nullptr) (void)hipFreeAsync(c->out[p], c->streams[p]);  // out and mm: one block
       c->out[p] = nullptr;
@@ -190,6 +208,8 @@ int leveldb_crc32c_batch_multi(int ndev, const int* devices, const void* const* 
                                 n[p], o, m, flags, c->streams[p]);
       if (rc != 0) return finish(rc);
     }
+    if ((e = hipSetDevice(devices[p])) != hipSuccess) return finish(HipFail(e, "hipSetDevice"));
+    if ((e = hipEventRecord(c->t1[p], c->streams[p])) != hipSuccess) return finish(HipFail(e, "hipEventRecord"));
     if (p == fail_after)
       return finish(MultiFail(PRISMDB_CRC32C_EDEVICE, "batch_multi: injected failure (test hook)"));
   }
@@ -214,12 +234,55 @@ int leveldb_crc32c_batch_multi(int ndev, const int* devices, const void* const* 
     if (r != ncclSuccess) return finish(NcclFail(r, "ncclSend/ncclRecv"));
     if (r2 != ncclSuccess) return finish(NcclFail(r2, "ncclGroupEnd"));
   }
+  for (int p = 0; p < ndev; ++p) {
+    if ((e = hipSetDevice(devices[p])) != hipSuccess) return finish(HipFail(e, "hipSetDevice"));
+    if ((e = hipEventRecord(c->t2[p], c->streams[p])) != hipSuccess) return finish(HipFail(e, "hipEventRecord"));
+  }
+  c->timed = true;
   // the caller's streams resume after the clique's work
   return finish(0);
 }
 
+// Diagnostics (not in the public header): the phases of the last successful
+// call on the clique of this device list, per device p, after waiting for it:
+// batch_ms[p] = its own batch (hand-off to batch end on its clique stream),
+// gather_ms[p] = batch end to the end of its part of the gather (on devices[0]:
+// until every partition has arrived); *init_ms = ncclCommInitAll's wall time
+// when the clique was created.  Read-only.  0; -1 if no such clique or call.
+int prismdb_crc32c_multi_timing(int ndev, const int* devices, float* batch_ms, float* gather_ms, double* init_ms) {
+  if (ndev < 1 || devices == nullptr) return -1;
+  Clique* c = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    for (Clique* x : g_cliques)
+      if ((int)x->devs.size() == ndev && std::memcmp(x->devs.data(), devices, sizeof(int) * ndev) == 0) c = x;
+  }
+  if (c == nullptr) return -1;
+  std::lock_guard<std::mutex> lk(c->mu);
+  if (init_ms != nullptr) *init_ms = c->init_ms;
+  if (!c->timed) return -1;
+  int cur = 0;
+  (void)hipGetDevice(&cur);
+  int rc = 0;
+  for (int p = 0; p < ndev && rc == 0; ++p) {
+    float b = 0, g = 0;
+    hipError_t e = hipSetDevice(devices[p]);
+    if (e == hipSuccess) e = hipEventSynchronize(c->t2[p]);
+    if (e == hipSuccess) e = hipEventElapsedTime(&b, c->t0[p], c->t1[p]);
+    if (e == hipSuccess) e = hipEventElapsedTime(&g, c->t1[p], c->t2[p]);
+    if (e != hipSuccess) rc = HipFail(e, "multi timing");
+    if (batch_ms != nullptr) batch_ms[p] = b;
+    if (gather_ms != nullptr) gather_ms[p] = g;
+  }
+  (void)hipSetDevice(cur);
+  return rc;
+}
+
 // Test hook (not in the public header): fail every call right after
 // partition p's batch is enqueued (-1: off); returns the previous value.
-int prismdb_crc32c_multi_fail_after(int p) { return g_fail_after.exchange(p < 0 ? -1 : p); }
+int prismdb_crc32c_multi_fail_after(int p) {
+  if (!prismdb::TestHooksEnabled()) return g_fail_after.load();  // (crc32c_capi.hip)
+  return g_fail_after.exchange(p < 0 ? -1 : p);
+}
 
 }  // extern "C"

@@ -37,6 +37,7 @@ void SetLastError(const std::string& msg);  // crc32c_capi.hip: leveldb_crc32c_l
 // (not one per thread that leases the ring), released with the ring
 void RegisterEngineStream(hipStream_t s);
 void ReleaseEngineStream(hipStream_t s);
+bool TestHooksEnabled();  // crc32c_capi.hip: PRISMDB_ENABLE_TEST_HOOKS
 }
 
 namespace {
@@ -241,17 +242,22 @@ int leveldb_crc32c_batch_host(const void* host_base, const uint64_t* off, const 
   if (n == 0) return 0;
   if (host_base == nullptr || off == nullptr || len == nullptr)
     return PipeFail(PRISMDB_CRC32C_EINVAL, "host_base/off/len must be non-NULL");
-  if (flags & ~(PRISMDB_CRC32C_MASK | PRISMDB_CRC32C_LOG_HEADER))
-    return PipeFail(PRISMDB_CRC32C_EINVAL, "host batches take PRISMDB_CRC32C_MASK and _LOG_HEADER only");
+  if (flags & ~(PRISMDB_CRC32C_MASK | PRISMDB_CRC32C_LOG_HEADER | PRISMDB_CRC32C_WRITE_TRAILER))
+    return PipeFail(PRISMDB_CRC32C_EINVAL, "host batches take PRISMDB_CRC32C_MASK, _WRITE_TRAILER and _LOG_HEADER only");
+  const bool seal = (flags & PRISMDB_CRC32C_WRITE_TRAILER) != 0;
+  if (seal && mismatch != nullptr)
+    return PipeFail(PRISMDB_CRC32C_EINVAL, "WRITE_TRAILER and verify are exclusive");
   // Verify reads the stored checksum: the 4 bytes after the span, or with
-  // LOG_HEADER the log record header 6 bytes before it.
+  // LOG_HEADER the log record header 6 bytes before it.  A seal writes it
+  // there on the host (below): those bytes never travel to the device.
   const bool hdr = (flags & PRISMDB_CRC32C_LOG_HEADER) != 0;
   const size_t lead = mismatch != nullptr && hdr ? 6 : 0;
   const size_t tail = mismatch != nullptr && !hdr ? 4 : 0;
   for (size_t i = 0; i < n; ++i) {
     if (lead + (size_t)len[i] + tail > kMaxSpan) return PipeFail(PRISMDB_CRC32C_EINVAL, "span larger than 64 MiB");
     if (i && off[i] < off[i - 1]) return PipeFail(PRISMDB_CRC32C_EINVAL, "spans must be sorted by offset");
-    if (off[i] < lead) return PipeFail(PRISMDB_CRC32C_EINVAL, "log record header before the buffer start");
+    if (off[i] < lead || (seal && hdr && off[i] < 6))
+      return PipeFail(PRISMDB_CRC32C_EINVAL, "log record header before the buffer start");
   }
   RingLease lease;
   int rc = lease.Acquire();
@@ -275,13 +281,30 @@ int leveldb_crc32c_batch_host(const void* host_base, const uint64_t* off, const 
   };
 
   // Retire a slot: wait until the compute stream released it, hand its
-  // results to the caller.
+  // results to the caller.  Sealing, the results are also stored into the
+  // caller's buffer as each span's trailer -- 4 LE bytes right behind it, or
+  // with LOG_HEADER the record header's crc 6 bytes before it -- where
+  // TableBuilder::WriteRawBlock appends them to its 32 MiB write buffer
+  // (table/table_builder.cc:192-197, util/env_posix.cc:279-309).  A chunk's
+  // trailers go out while the next kDepth - 1 chunks are in flight.  (Left to
+  // the caller after the call, 1.93 M scattered stores cost config 4's write
+  // leg 12 % against its read leg: bench.py compaction_leg, round 4.)
+  uint8_t* const dst = static_cast<uint8_t*>(const_cast<void*>(host_base));
   auto retire = [&](Slot& s) -> int {
     if (!s.busy) return 0;
     hipError_t e = hipEventSynchronize(s.done);
     if (e != hipSuccess) return PipeFail(PRISMDB_CRC32C_EDEVICE, std::string("pipeline: ") + hipGetErrorString(e));
     if (out) std::memcpy(out + s.first, s.h_out, s.count * 4);
     if (mismatch) std::memcpy(mismatch + s.first, s.h_mm, s.count);
+    if (seal) {
+      const uint64_t* o = off + s.first;
+      const uint32_t* l = len + s.first;
+      if (hdr) {
+        for (size_t q = 0; q < s.count; ++q) std::memcpy(dst + o[q] - 6, s.h_out + q, 4);
+      } else {
+        for (size_t q = 0; q < s.count; ++q) std::memcpy(dst + o[q] + l[q], s.h_out + q, 4);
+      }
+    }
     s.busy = false;
     return 0;
   };
@@ -332,7 +355,8 @@ int leveldb_crc32c_batch_host(const void* host_base, const uint64_t* off, const 
     rc = fail_after > 0 && ++chunks >= fail_after
              ? PipeFail(PRISMDB_CRC32C_EDEVICE, "pipeline: injected failure (prismdb_pipeline_fail_after)")
              : leveldb_crc32c_batch(s.d_data, d_off, d_len, init ? d_init : nullptr, cnt, s.d_out,
-                                    mismatch ? s.d_mm : nullptr, flags, ring->compute);
+                                    mismatch ? s.d_mm : nullptr, flags & ~PRISMDB_CRC32C_WRITE_TRAILER,
+                                    ring->compute);
     if (rc != 0) return abort_call(rc);  // message already set by leveldb_crc32c_batch
     e = hipMemcpyAsync(s.h_out, s.d_out, cnt * 4, hipMemcpyDeviceToHost, ring->compute);
     if (e == hipSuccess && mismatch) e = hipMemcpyAsync(s.h_mm, s.d_mm, cnt, hipMemcpyDeviceToHost, ring->compute);
@@ -350,12 +374,14 @@ int leveldb_crc32c_batch_host(const void* host_base, const uint64_t* off, const 
   return 0;
 }
 
-void prismdb_pipeline_fail_after(int chunks) { g_fail_after_chunks.store(chunks > 0 ? chunks : 0, std::memory_order_relaxed); }
+void prismdb_pipeline_fail_after(int chunks) {
+  if (prismdb::TestHooksEnabled()) g_fail_after_chunks.store(chunks > 0 ? chunks : 0, std::memory_order_relaxed);
+}
 
 // Tuning hook: chunk size of later host batches (0: leave it; clamped to
 // [1 MiB, kMaxSpan]); returns the previous value.
 size_t prismdb_pipeline_chunk_bytes(size_t bytes) {
-  if (bytes == 0) return g_chunk_bytes.load(std::memory_order_relaxed);
+  if (bytes == 0 || !prismdb::TestHooksEnabled()) return g_chunk_bytes.load(std::memory_order_relaxed);
   const size_t b = bytes < (1u << 20) ? (1u << 20) : (bytes > kMaxSpan ? kMaxSpan : bytes);
   return g_chunk_bytes.exchange(b, std::memory_order_relaxed);
 }

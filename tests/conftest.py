@@ -10,6 +10,11 @@ import subprocess
 
 import pytest
 
+# The library's prismdb_* routing and fault-injection setters act only in a
+# process started with this (crc32c_capi.hip, TestHooksEnabled); the tests pin
+# routes with them.  Set before the library's first hook call.
+os.environ.setdefault("PRISMDB_ENABLE_TEST_HOOKS", "1")
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GOLD = os.path.join(ROOT, "tests", "golden")
 ORACLE_SO = os.path.join(ROOT, "oracle", "_build", "liboracle.so")

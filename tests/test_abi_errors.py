@@ -74,8 +74,17 @@ def test_host_batch_checks(native, bufs):
     data, off, ln, out, mm = bufs
     p = data.ctypes.data
     assert native.leveldb_crc32c_batch_host(p, off.ctypes.data, ln.ctypes.data, None, 4, out.ctypes.data, None,
-                                            WRITE_TRAILER) == EINVAL
+                                            0x8) == EINVAL  # UNORDERED: device batches only
     assert "MASK" in _err(native)
+    # WRITE_TRAILER seals host buffers, but not while verifying
+    assert native.leveldb_crc32c_batch_host(p, off.ctypes.data, ln.ctypes.data, None, 4, out.ctypes.data,
+                                            mm.ctypes.data, WRITE_TRAILER) == EINVAL
+    assert "exclusive" in _err(native)
+    # a log-record seal writes 6 bytes before each span
+    off2 = np.array([3, 4096], dtype=np.uint64)
+    assert native.leveldb_crc32c_batch_host(p, off2.ctypes.data, ln.ctypes.data, None, 2, out.ctypes.data, None,
+                                            WRITE_TRAILER | LOG_HEADER) == EINVAL
+    assert "header" in _err(native)
     unsorted = off[::-1].copy()
     assert native.leveldb_crc32c_batch_host(p, unsorted.ctypes.data, ln.ctypes.data, None, 4, out.ctypes.data,
                                             None, 0) == EINVAL
@@ -170,3 +179,30 @@ def test_multi_argument_checks(native, bufs):
     assert _multi(native, 1, [0], [b], [o], [l], [4], po, flags=0x10) == EINVAL and "flag" in _err(native)
     assert _multi(native, 1, [0], [b], [o], [l], [4], po, mm.ctypes.data, WRITE_TRAILER) == EINVAL
     assert "exclusive" in _err(native)
+
+
+def test_test_hooks_gated_by_environment():
+    """The prismdb_* routing and fault-injection setters are process-global:
+    without PRISMDB_ENABLE_TEST_HOOKS=1 they change nothing (a PrismDB
+    partition thread cannot reroute or fail the others' batches) and report
+    the current setting; with it they act.  Run in fresh processes (the
+    switch is read once)."""
+    import os
+    import subprocess
+    import sys
+
+    code = ("import ctypes, sys; L = ctypes.CDLL(sys.argv[1]); L.prismdb_crc32c_direct_max.restype = ctypes.c_uint64; "
+            "L.prismdb_crc32c_direct_max.argtypes = [ctypes.c_uint64]; L.prismdb_crc32c_windows.argtypes = [ctypes.c_int]; "
+            "a = L.prismdb_crc32c_direct_max(5); b = L.prismdb_crc32c_direct_max(7); "
+            "w = L.prismdb_crc32c_windows(0); w2 = L.prismdb_crc32c_windows(1); "
+            "print(L.prismdb_test_hooks_enabled(), a, b, w, w2)")
+    from prismdb_amd import _lib
+
+    for flag, want in ((None, "0 131072 131072 2 2"), ("1", "1 131072 5 2 0")):
+        env = {k: v for k, v in os.environ.items() if k != "PRISMDB_ENABLE_TEST_HOOKS"}
+        if flag:
+            env["PRISMDB_ENABLE_TEST_HOOKS"] = flag
+        r = subprocess.run([sys.executable, "-c", code, _lib.LIB_PATH], env=env, capture_output=True, text=True,
+                           timeout=120)
+        assert r.returncode == 0, r.stderr
+        assert r.stdout.strip() == want, (flag, r.stdout, r.stderr)

@@ -686,6 +686,100 @@ def test_host_pipeline_mixed_large_spans(dev, oracle, pipe_chunk):
     assert np.nonzero(mm)[0].tolist() == [302]
 
 
+def _sealed_image(oracle, host, off, lens, log_header=False):
+    """The oracle's sealed copy of `host`: every span's Mask(Value(span))
+    stored as 4 LE bytes after it (TableBuilder::WriteRawBlock,
+    table/table_builder.cc:192-197) or, for log records, 6 bytes before it
+    (log::Writer::EmitPhysicalRecord, db/log_writer.cc:90-97)."""
+    want = host.copy()
+    crc, _ = oracle.batch(host, off, lens, mask=True)
+    at = (off.astype(np.int64) - 6) if log_header else (off.astype(np.int64) + lens.astype(np.int64))
+    want[at[:, None] + np.arange(4)[None, :]] = crc.astype("<u4").view(np.uint8).reshape(-1, 4)
+    return want, crc
+
+
+@pytest.mark.parametrize("pinned", [False, True])
+def test_host_pipeline_seal_trailers(dev, oracle, pinned):
+    """leveldb_crc32c_batch_host with WRITE_TRAILER: a 152 MiB SST-shaped
+    image (3988-B contents||type spans at stride 3992, three 64 MiB chunks)
+    with zeroed trailers, pageable and pinned: afterwards every byte of the
+    buffer equals the oracle-sealed image, and the returned crcs are the
+    masked values; a verify pass over the result flags nothing."""
+    import torch
+    from prismdb_amd import crc32c
+
+    n = 40000
+    off = np.arange(n, dtype=np.uint64) * 3992
+    lens = np.full(n, 3988, dtype=np.uint32)
+    img = oracle.synth(n * 3992 + 8, 0x5EED0013)
+    img[(off + 3988).astype(np.int64)[:, None] + np.arange(4)[None, :]] = 0
+    want, crc = _sealed_image(oracle, img, off, lens)
+    host = torch.from_numpy(img.copy()).pin_memory() if pinned else img.copy()
+    got, _ = crc32c.batch_host(host, off, lens, mask=True, trailer=True)
+    np.testing.assert_array_equal(got, crc)
+    after = host.numpy() if pinned else host
+    assert (after == want).all(), np.nonzero(after != want)[0][:8]
+    _, mm = crc32c.batch_host(host, off, lens, verify=True)
+    assert int(mm.sum()) == 0
+
+
+def test_host_pipeline_seal_log_headers(dev, oracle, pipe_chunk32):
+    """WRITE_TRAILER | LOG_HEADER on the host path: log records of 0..1280
+    payload bytes (span = type||payload) at odd offsets over several 32 MiB
+    chunks; the header crc 6 bytes before each span is written and nothing
+    else changes."""
+    from prismdb_amd import crc32c
+
+    rng = np.random.default_rng(0x5EED0014)
+    lens = rng.integers(1, 1282, size=60000).astype(np.uint32)
+    off = np.empty(len(lens), dtype=np.uint64)
+    pos = 13
+    for i, ln in enumerate(lens):
+        off[i] = pos + 6  # crc[4] length[2] | type||payload
+        pos += 6 + int(ln) + int(rng.integers(0, 9))
+    img = oracle.synth(pos + 16, 0x5EED0015)
+    want, crc = _sealed_image(oracle, img, off, lens, log_header=True)
+    host = img.copy()
+    got, _ = crc32c.batch_host(host, off, lens, mask=True, trailer=True, log_header=True)
+    np.testing.assert_array_equal(got, crc)
+    assert (host == want).all(), np.nonzero(host != want)[0][:8]
+
+
+def test_host_pipeline_seal_failure_drains(dev, oracle, pipe_chunk32):
+    """A sealing host batch that fails after chunks are in flight returns an
+    error, writes no trailer past the chunks it finished, and the next sealing
+    call (same ring) seals the whole image exactly."""
+    import ctypes
+
+    from prismdb_amd import _lib, crc32c
+
+    L = _lib.lib()
+    L.prismdb_pipeline_fail_after.argtypes = [ctypes.c_int]
+    n = 40000
+    off = np.arange(n, dtype=np.uint64) * 3992
+    lens = np.full(n, 3988, dtype=np.uint32)
+    img = oracle.synth(n * 3992 + 8, 0x5EED0016)
+    tr = (off + 3988).astype(np.int64)[:, None] + np.arange(4)[None, :]
+    img[tr] = 0
+    want, _ = _sealed_image(oracle, img, off, lens)
+    host = img.copy()
+    L.prismdb_pipeline_fail_after(3)
+    try:
+        with pytest.raises(RuntimeError, match="injected failure"):
+            crc32c.batch_host(host, off, lens, mask=True, trailer=True)
+    finally:
+        L.prismdb_pipeline_fail_after(0)
+    # spans outside the trailers never change; trailers are either still zero
+    # or already their sealed value (chunks finished before the failure)
+    body = np.ones(host.size, dtype=bool)
+    body[tr.reshape(-1)] = False
+    assert (host[body] == img[body]).all()
+    t_got, t_want = host[tr], want[tr]
+    assert ((t_got == 0).all(axis=1) | (t_got == t_want).all(axis=1)).all()
+    crc32c.batch_host(host, off, lens, mask=True, trailer=True)
+    assert (host == want).all()
+
+
 @pytest.fixture
 def pipe_chunk32():
     """32 MiB host pipeline chunks for the test (the default is 64 MiB)."""

@@ -16,6 +16,7 @@ import statistics
 import subprocess
 import sys
 
+os.environ.setdefault("PRISMDB_ENABLE_TEST_HOOKS", "1")  # the library's prismdb_* setters act only with this
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 SO = os.path.join(ROOT, "tools", "_build", "libbwprobe.so")

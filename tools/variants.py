@@ -25,8 +25,10 @@ import json
 import os
 import shutil
 import statistics
+import subprocess
 import sys
 
+os.environ.setdefault("PRISMDB_ENABLE_TEST_HOOKS", "1")  # the library's prismdb_* setters act only with this
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 VDIR = os.environ.get("PRISMDB_VLIB", os.path.join(ROOT, "tools", "vlib"))  # (override: trial builds)
@@ -94,16 +96,16 @@ VARIANTS = {
          "    reinterpret_cast<uint64_t*>(a.out + ((n + 3u) & ~3u))[8u * wave + lane] = v;\n  }\n}\n\nhipError_t launch_direct"),
     ] + MEASURE_ONLY,
     # the one-launch kernel before round 4's ring change: two slots of three
-    # streams (tools/patches/crc32c_direct_r03.hip, the round-3 source)
-    "ring6": [("crc32c_direct.hip", "@file", "tools/patches/crc32c_direct_r03.hip")],
+    # streams (the round-3 source, from git history)
+    "ring6": [("crc32c_direct.hip", "@git", "bab2234:prismdb_amd/csrc/crc32c_direct.hip")],
     # round 4's first ring: one task sequence only, whatever the batch size
-    "ring4": [("crc32c_direct.hip", "@file", "tools/patches/crc32c_direct_ring4.hip")],
+    "ring4": [("crc32c_direct.hip", "@git", "83d3f73:prismdb_amd/csrc/crc32c_direct.hip")],
     # two slots of two streams (positions mod 2): a fold waits for two tasks
-    # and runs two LDS chains (tools/patches/crc32c_direct_ring22.hip)
-    "ring22": [("crc32c_direct.hip", "@file", "tools/patches/crc32c_direct_ring22.hip")],
+    # and runs two LDS chains (a measurement copy kept in round 4's tree)
+    "ring22": [("crc32c_direct.hip", "@git", "2cab585:tools/patches/crc32c_direct_ring22.hip")],
     # the ring before two single-task slots: four slots, and two task
-    # sequences in pairs for short runs (tools/patches/crc32c_direct_slots4.hip)
-    "slots4": [("crc32c_direct.hip", "@file", "tools/patches/crc32c_direct_slots4.hip")],
+    # sequences in pairs for short runs
+    "slots4": [("crc32c_direct.hip", "@git", "8295f55:prismdb_amd/csrc/crc32c_direct.hip")],
     # the one-launch kernel at 16 waves per CU (1024-thread groups; needs
     # <= 128 VGPRs): fewer tasks per wave, so a wave's chain of folds ends sooner
     "w16": [("crc32c_device.h", "constexpr int kDirectThreads = 768;", "constexpr int kDirectThreads = 1024;")],
@@ -286,8 +288,9 @@ def do_build(names):
             os.symlink(os.path.join(ROOT, "include"), inc)
         for fname, old, new in spec:
             path = os.path.join(src, fname)
-            if old == "@file":  # (fname, "@file", path): the whole file replaced by a copy under tools/patches
-                shutil.copyfile(os.path.join(ROOT, new), path)
+            if old == "@git":  # (fname, "@git", "rev:path"): the whole file as it was at a commit
+                with open(path, "wb") as f:
+                    f.write(subprocess.check_output(["git", "-C", ROOT, "show", new]))
                 continue
             with open(path) as f:
                 text = f.read()
