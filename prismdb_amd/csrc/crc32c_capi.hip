@@ -273,6 +273,8 @@ struct Workspace {
   uint32_t cap_streams = 0;  // the span-kernel streams the slice starts of `grow` were sized for
   char* qgrow = nullptr;
   size_t cap_q = 0;
+  char* sgrow = nullptr;  // sealing planner batches without `out`: their results for the trailer pass
+  size_t cap_s = 0;
   char* direct = nullptr;  // word, done | ticket map | partials | per-span counters
   uint32_t gen = 0;
   bool owned = false;  // an engine stream's (g_owned), not a thread's
@@ -297,7 +299,7 @@ void SyncAndRelease(Workspace& w) {
     if (ev != nullptr) (void)hipEventSynchronize(ev);
   const hipStream_t rs = g_ctx[w.device].release;
   for (void* blk : {static_cast<void*>(w.mem), static_cast<void*>(w.grow), static_cast<void*>(w.qgrow),
-                    static_cast<void*>(w.direct)})
+                    static_cast<void*>(w.sgrow), static_cast<void*>(w.direct)})
     if (blk != nullptr) (void)hipFreeAsync(blk, rs);
   (void)hipStreamSynchronize(rs);
   hipMemPool_t pool = nullptr;
@@ -654,7 +656,23 @@ int RunBatch(DeviceCtx& ctx, const SpanBatch& base_args, bool desc, bool verify,
   t_last_direct = false;
   t_last_owned = w->owned;
   t_last_epoch = g_release_epoch.load(std::memory_order_acquire);
-  uint32_t* const caller_out = a.out;
+  // Sealing: the lane and span kernels leave the trailers to one pass after
+  // them (crc32c_trailer_kernel), which reads the results back -- from
+  // scratch when the caller passed no `out`.
+  const bool trailer_pass = (a.flags & prismdb::dev::kFlagWriteTrailer) != 0;
+  if (trailer_pass) {
+    a.flags &= ~prismdb::dev::kFlagWriteTrailer;
+    if (a.out == nullptr) {
+      if (w->cap_s < a.n) {
+        const size_t cap = a.n < 4096 ? 4096 : a.n + a.n / 4;
+        w->cap_s = 0;
+        if ((rc = GrowBlock(&w->sgrow, cap * 4, s, "trailer result workspace")) != 0) return rc;
+        w->cap_s = cap;
+      }
+      a.out = reinterpret_cast<uint32_t*>(w->sgrow);
+    }
+  }
+  uint32_t* const res_out = a.out;  // the caller's out, or the trailer pass's scratch
   uint8_t* const caller_mm = a.mismatch;
   if (lane) {
     a.qrun = ws.qrun;
@@ -707,10 +725,16 @@ int RunBatch(DeviceCtx& ctx, const SpanBatch& base_args, bool desc, bool verify,
   if (e != hipSuccess) return FailHip(e, "combine kernel launch");
   if (lane) {
     SpanBatch back = a;
-    back.out = caller_out;
+    back.out = res_out;
     back.mismatch = caller_mm;
     e = prismdb::dev::launch_scatter(back, ws, ws.qout, ws.qmm, s);
     if (e != hipSuccess) return FailHip(e, "scatter kernel launch");
+  }
+  if (trailer_pass) {
+    SpanBatch t = base_args;
+    t.n = a.n;
+    e = prismdb::dev::launch_trailers(t, desc, res_out, s);
+    if (e != hipSuccess) return FailHip(e, "trailer kernel launch");
   }
   return 0;
 }

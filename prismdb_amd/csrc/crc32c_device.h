@@ -191,6 +191,9 @@ hipError_t launch_direct(const SpanBatch& a, bool verify, int grid, const Direct
                          hipEvent_t done);
 hipError_t launch_scatter(const SpanBatch& a, const SplitWs& ws, const uint32_t* qout, const uint8_t* qmm,
                           hipStream_t s);
+// WRITE_TRAILER on the planner path: every span's trailer from res[i], after
+// the span kernels (crc32c_trailer_kernel).
+hipError_t launch_trailers(const SpanBatch& a, bool desc, const uint32_t* res, hipStream_t s);
 
 }  // namespace dev
 }  // namespace prismdb

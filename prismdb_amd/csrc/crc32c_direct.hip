@@ -188,6 +188,10 @@ constexpr uint32_t kHelpChunks = 256;
 // ticks, 100 MHz): 3 us.  Pushes come right after the static waves' first
 // descriptor loads (~1.5-2.5 us into the kernel).
 constexpr uint64_t kHelpPoll = 300u;
+// Static-run weights of a group's waves 0-3, 4-7 and 8-11 (one per SIMD each;
+// see the run deal in the kernel).
+constexpr uint32_t kRunWeight[3] = {1u, 1u, 1u};
+static_assert(kDirectWaves == 12u, "the run weights assume 12 waves per group, 3 per SIMD");
 static_assert(kDirectMaxSpans < kNullEntry, "span indices fit the entry's 24-bit field");
 
 template <bool kVerify>
@@ -218,9 +222,28 @@ __global__ __launch_bounds__(kDirectThreads) void crc32c_direct_kernel(SpanBatch
   const bool worker = wave >= nwaves - workers;
   uint32_t sbase = 0, m = 0;
   if (wave < K) {
-    const uint32_t q = n / K, r = n % K;
-    sbase = wave * q + (wave < r ? wave : r);
-    m = q + (wave < r ? 1u : 0u);
+    // Runs weighted by the wave's place in its group: wave k of a group
+    // shares its SIMD (k mod 4) with two others, and the older ones issue
+    // first -- a file-sized call's waves 0-3 / 4-7 / 8-11 drained at 11.5 /
+    // 12.3 / 13.4 us with the same six spans each (tools/direct_timeline.py,
+    // profiles/r05/r05b_timeline_groups.json).  Group g's spans stay
+    // consecutive; unweighted when the groups are not all whole or a run
+    // would pass 64 spans.
+    constexpr uint32_t kW0 = kRunWeight[0], kW1 = kRunWeight[1], kW2 = kRunWeight[2];
+    constexpr uint32_t kWg = 4u * (kW0 + kW1 + kW2), kWmax = kW0 > kW1 ? (kW0 > kW2 ? kW0 : kW2) : (kW1 > kW2 ? kW1 : kW2);
+    const uint64_t tot = (uint64_t)(K / kDirectWaves) * kWg;
+    if (K % kDirectWaves == 0u && (uint64_t)n * kWmax <= 63ull * tot) {
+      const uint32_t g = wave / kDirectWaves, k = wave % kDirectWaves;
+      const uint32_t wk = k < 4u ? kW0 : (k < 8u ? kW1 : kW2);
+      const uint32_t cum = k < 4u ? k * kW0 : (k < 8u ? 4u * kW0 + (k - 4u) * kW1 : 4u * (kW0 + kW1) + (k - 8u) * kW2);
+      const uint64_t at = (uint64_t)g * kWg + cum;
+      sbase = (uint32_t)((uint64_t)n * at / tot);
+      m = (uint32_t)((uint64_t)n * (at + wk) / tot) - sbase;
+    } else {
+      const uint32_t q = n / K, r = n % K;
+      sbase = wave * q + (wave < r ? wave : r);
+      m = q + (wave < r ? 1u : 0u);
+    }
   }
   // A group works if any of its waves has a run or is a ticket worker
   // (adopted tickets and whole spans belong to waves with a run).  The

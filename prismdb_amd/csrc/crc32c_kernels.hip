@@ -1421,6 +1421,32 @@ __global__ __launch_bounds__(256) void crc32c_scatter_kernel(SpanBatch a, SplitW
 }
 
 // ---------------------------------------------------------------------------
+// Trailer pass of a sealing planner-path batch: span i's result (out[i],
+// already Mask()ed with MASK) as 4 LE bytes right after it, or with
+// LOG_HEADER 6 bytes before it (TableBuilder::WriteRawBlock,
+// table/table_builder.cc:192-197; log::Writer, db/log_writer.cc:90-97).  The
+// span and pair kernels could store each run's trailers themselves, but
+// scattered 4-byte writes spread through the read stream cost the pair
+// kernel 17 % on bulk SST seals (4954 against 5966 GB/s without the stores,
+// whatever their cache policy: profiles/r05/r05b_variants_pair_seal.json);
+// the one-launch kernel, whose trailers go out together at the end of each
+// wave's run, seals almost free.  So the trailers of a bulk batch go out
+// here, in one burst after the reads: one thread per span, descriptors and
+// results read coalesced.
+// ---------------------------------------------------------------------------
+template <bool kDesc>
+__global__ __launch_bounds__(256) void crc32c_trailer_kernel(SpanBatch a, const uint32_t* res) {
+  const bool hdr = (a.flags & kFlagLogHeader) != 0;
+  const uint64_t step = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += step) {
+    const uint64_t off = kDesc ? a.off[i] : i * a.stride;
+    const uint32_t len = kDesc ? a.len[i] : a.len_c;
+    const uint8_t* t = hdr ? a.base + off - kLogCrcBack : a.base + off + len;
+    store_le32(t, res[i]);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Host-side launchers (called from crc32c_capi.hip through crc32c_device.h).
 // ---------------------------------------------------------------------------
 hipError_t launch_span(const SpanBatch& a, bool verify, int grid, hipStream_t s) {
@@ -1485,6 +1511,14 @@ hipError_t launch_lane(const SpanBatch& a, bool verify, int grid, const SplitWs&
 hipError_t launch_scatter(const SpanBatch& a, const SplitWs& ws, const uint32_t* qout, const uint8_t* qmm,
                           hipStream_t s) {
   crc32c_scatter_kernel<<<256, 256, 0, s>>>(a, ws, qout, qmm);
+  return hipGetLastError();
+}
+
+hipError_t launch_trailers(const SpanBatch& a, bool desc, const uint32_t* res, hipStream_t s) {
+  const uint64_t blocks = (a.n + 255u) / 256u;
+  const int grid = (int)(blocks < 16384u ? blocks : 16384u);
+  if (desc) crc32c_trailer_kernel<true><<<grid, 256, 0, s>>>(a, res);
+  else crc32c_trailer_kernel<false><<<grid, 256, 0, s>>>(a, res);
   return hipGetLastError();
 }
 

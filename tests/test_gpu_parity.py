@@ -250,6 +250,73 @@ def test_pair_run_schedule(dev, oracle, native, n, bulk_route):
     np.testing.assert_array_equal(sbuf.cpu().numpy(), want)
 
 
+def test_planner_seal_trailer_pass_without_out(dev, oracle, native, planner_bulk):
+    """A sealing planner-path batch (300 001 spans: the pair-run kernel, long
+    spans through the segment pass) with out = NULL: the trailer pass reads
+    the results from the workspace's scratch.  Every trailer is the masked
+    crc, no other byte moves; LOG_HEADER seals (header crc 6 bytes before
+    each span) the same way on the span-only route."""
+    import torch
+
+    n = 300001
+    rng = np.random.default_rng(0x5EED0042)
+    lens = rng.integers(0, 4097, size=n).astype(np.int64)
+    lens[5::1999] = rng.integers(131073, 300000, size=len(lens[5::1999]))
+    off = np.concatenate([[19], 19 + np.cumsum(lens + 4 + 6 + rng.integers(0, 5, size=n))[:-1]]).astype(np.uint64)
+    size = int(off[-1] + lens[-1] + 4 + 8)
+    host = oracle.synth(size, 0x5EED0043)
+    masked, _ = oracle.batch(host, off, lens.astype(np.uint32), mask=True)
+    d_off = torch.from_numpy(off.astype(np.int64)).to(dev)
+    d_len = torch.from_numpy(lens.astype(np.uint32).view(np.int32)).to(dev)
+    native.leveldb_crc32c_last_error.restype = ctypes.c_char_p
+    for hdr in (False, True):
+        prev = native.prismdb_crc32c_lane_mode(-1) if hdr else None  # log records without the lane kernel
+        try:
+            at = (off.astype(np.int64) - 6) if hdr else (off + lens.astype(np.uint64)).astype(np.int64)
+            tr = at[:, None] + np.arange(4)[None, :]
+            img = host.copy()
+            img[tr] = 0
+            buf = torch.from_numpy(img).to(dev)
+            rc = native.leveldb_crc32c_batch(ctypes.c_void_p(buf.data_ptr()), ctypes.c_void_p(d_off.data_ptr()),
+                                             ctypes.c_void_p(d_len.data_ptr()), None, ctypes.c_size_t(n), None, None,
+                                             ctypes.c_uint32(0x3 | (0x4 if hdr else 0)),
+                                             ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+            assert rc == 0, native.leveldb_crc32c_last_error()
+            want = img.copy()
+            want[tr] = masked.astype("<u4").view(np.uint8).reshape(-1, 4)
+            got = buf.cpu().numpy()
+            assert (got == want).all(), (hdr, np.nonzero(got != want)[0][:8])
+        finally:
+            if hdr:
+                native.prismdb_crc32c_lane_mode(0)
+
+
+@pytest.mark.parametrize("n", [1000, 300000])
+def test_fixed_stride_seal(dev, oracle, native, n):
+    """leveldb_crc32c_batch_fixed with MASK | WRITE_TRAILER (the generic path
+    and its trailer pass: 4092-B contents||type blocks at stride 4096, and
+    3987-B blocks at an odd stride), trailers zeroed first: afterwards every
+    byte equals the oracle-sealed image and out holds the masked crcs."""
+    import torch
+
+    for stride, length in ((4096, 4092), (3993, 3987)):
+        img = oracle.synth(n * stride + 8, 0x5EED0044 + stride)
+        off = np.arange(n, dtype=np.uint64) * stride
+        tr = (off + length).astype(np.int64)[:, None] + np.arange(4)[None, :]
+        img[tr] = 0
+        masked, _ = oracle.batch(img, off, np.full(n, length, dtype=np.uint32), mask=True)
+        buf = torch.from_numpy(img).to(dev)
+        out = torch.empty(n, dtype=torch.int32, device=dev)
+        rc = native.leveldb_crc32c_batch_fixed(ctypes.c_void_p(buf.data_ptr()), stride, length, n, 0,
+                                               ctypes.c_void_p(out.data_ptr()), None, ctypes.c_uint32(0x3),
+                                               ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+        assert rc == 0
+        np.testing.assert_array_equal(_u32(out), masked)
+        want = img.copy()
+        want[tr] = masked.astype("<u4").view(np.uint8).reshape(-1, 4)
+        assert (buf.cpu().numpy() == want).all(), (stride, length)
+
+
 def test_max_length_span(dev, oracle, native, route):
     """The longest span a descriptor holds (len = 2^32 - 1) at an odd offset,
     with an initial value, Mask and VERIFY against its stored trailer, next to

@@ -72,6 +72,29 @@ def main():
         v = v[ts[run, k] != 0]
         if len(v):
             res[name] = {p: round(float(np.percentile(v, p)), 2) for p in (0, 10, 50, 90, 100)}
+    # Where the drain spread lives: within a group (one CU's 12 waves), across
+    # groups, or across XCDs (group g runs on XCD g % 8: workgroups are dealt
+    # round-robin over the XCDs).
+    g = np.arange(nwaves) // 12
+    dr = rel[:, 5]
+    ok = run & (ts[:, 5] != 0)
+    gmax, gmin, gmean, xs = [], [], [], {x: [] for x in range(8)}
+    for grp in np.unique(g[ok]):
+        v = dr[ok & (g == grp)]
+        gmax.append(v.max())
+        gmin.append(v.min())
+        gmean.append(v.mean())
+        xs[int(grp) % 8].extend(v.tolist())
+    gmax, gmin, gmean = np.array(gmax), np.array(gmin), np.array(gmean)
+    res["drain_by_group"] = {
+        "group_max": {p: round(float(np.percentile(gmax, p)), 2) for p in (0, 10, 50, 90, 100)},
+        "group_mean": {p: round(float(np.percentile(gmean, p)), 2) for p in (0, 10, 50, 90, 100)},
+        "within_group_range_mean": round(float((gmax - gmin).mean()), 2),
+        "xcd_mean": [round(float(np.mean(xs[x])), 2) if xs[x] else None for x in range(8)],
+        "wave_in_group_mean": [round(float(dr[ok & (np.arange(nwaves) % 12 == k)].mean()), 2) for k in range(12)],
+    }
+    m = ts[:, 7]
+    res["drain_by_run_length"] = {int(k): round(float(dr[ok & (m == k)].mean()), 2) for k in np.unique(m[ok])}
     print(json.dumps(res))
 
 

@@ -234,6 +234,38 @@ VARIANTS = {
         ("crc32c_kernels.hip", '    asm volatile("" : "+v"(HD[sl]), "+v"(ED[sl]), "+v"(SC[sl]));\n',
          '    asm volatile("" : "+v"(HD[sl]), "+v"(ED[sl]), "+v"(SC[sl]), "+v"(SA[sl]), "+v"(SB[sl]));\n'),
     ],
+    # measurement-only (trailers not written): the pair-run kernel sealing
+    # without its once-per-run trailer stores -- what they cost on bulk SST seals
+    "pair_noseal": [("crc32c_kernels.hip",
+                     "        if (seal && ta != 0u) store_le32(reinterpret_cast<const uint8_t*>(ta), res);\n",
+                     "        (void)ta;\n")] + MEASURE_ONLY,
+    # the pair kernel's trailer stores plain (no nt) / write-through (sc0 sc1)
+    "pair_st_plain": [("crc32c_kernels.hip",
+                       "        if (seal && ta != 0u) store_le32(reinterpret_cast<const uint8_t*>(ta), res);\n",
+                       "        if (seal && ta != 0u) asm volatile(\"global_store_dword %0, %1, off\" : : \"v\"(ta), \"v\"(res) : \"memory\");\n")],
+    "pair_st_sc": [("crc32c_kernels.hip",
+                    "        if (seal && ta != 0u) store_le32(reinterpret_cast<const uint8_t*>(ta), res);\n",
+                    "        if (seal && ta != 0u) asm volatile(\"global_store_dword %0, %1, off sc0 sc1\" : : \"v\"(ta), \"v\"(res) : \"memory\");\n")],
+    # the one-launch kernel's static runs weighted by the wave's place in its
+    # group (waves 0-3 / 4-7 / 8-11)
+    "w543": [("crc32c_direct.hip", "constexpr uint32_t kRunWeight[3] = {1u, 1u, 1u};",
+              "constexpr uint32_t kRunWeight[3] = {5u, 4u, 3u};")],
+    "w654": [("crc32c_direct.hip", "constexpr uint32_t kRunWeight[3] = {1u, 1u, 1u};",
+              "constexpr uint32_t kRunWeight[3] = {6u, 5u, 4u};")],
+    "w765": [("crc32c_direct.hip", "constexpr uint32_t kRunWeight[3] = {1u, 1u, 1u};",
+              "constexpr uint32_t kRunWeight[3] = {7u, 6u, 5u};")],
+    # the one-launch ring raising the priority of waves with more ring spans
+    # left (s_setprio 0-3 by spans not yet started, after every issue)
+    "prio": [("crc32c_direct.hip",
+              "          tk[q] = static_task(jc, tk[q ^ 1]);\n          issue(tk[q], wb[q], eb[q]);\n",
+              "          tk[q] = static_task(jc, tk[q ^ 1]);\n          issue(tk[q], wb[q], eb[q]);\n"
+              "          {\n"
+              "            const uint32_t rem = (uint32_t)__popcll(shortm & (jc >= 64u ? 0ull : ~0ull << jc));\n"
+              "            if (rem >= 3u) __builtin_amdgcn_s_setprio(3);\n"
+              "            else if (rem == 2u) __builtin_amdgcn_s_setprio(2);\n"
+              "            else if (rem == 1u) __builtin_amdgcn_s_setprio(1);\n"
+              "            else __builtin_amdgcn_s_setprio(0);\n"
+              "          }\n")],
 }
 
 # the previous commit's kernels (a git worktree under build/:
@@ -261,6 +293,12 @@ VARIANTS["walsafe"] = [
      "      }\n"),
 ]
 # combinations
+VARIANTS["w876"] = [("crc32c_direct.hip", "constexpr uint32_t kRunWeight[3] = {1u, 1u, 1u};",
+                     "constexpr uint32_t kRunWeight[3] = {8u, 7u, 6u};")]
+VARIANTS["w765prio"] = VARIANTS["w765"] + VARIANTS["prio"]
+VARIANTS["w654prio"] = VARIANTS["w654"] + VARIANTS["prio"]
+VARIANTS["ts_w765"] = VARIANTS["direct_ts"] + VARIANTS["w765"]
+VARIANTS["ts_w765prio"] = VARIANTS["direct_ts"] + VARIANTS["w765"] + VARIANTS["prio"]
 
 
 def do_build(names):
