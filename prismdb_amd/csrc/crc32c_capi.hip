@@ -267,6 +267,11 @@ struct Workspace {
   // calls alternate between two slots; the planner path marks done[gen & 1]):
   // waiting for both covers everything that used the workspace.
   hipEvent_t done[2] = {nullptr, nullptr};
+  // The planner path's side stream (created on first use): the segment pass
+  // runs there, concurrently with the span kernel, between a fork and a join
+  // event on the batch's stream.
+  hipStream_t side = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
   void* mem = nullptr;
   char* grow = nullptr;
   size_t cap_rec = 0;
@@ -305,6 +310,12 @@ void SyncAndRelease(Workspace& w) {
   hipMemPool_t pool = nullptr;
   if (hipDeviceGetDefaultMemPool(&pool, w.device) == hipSuccess) (void)hipMemPoolTrimTo(pool, 0);
   for (hipEvent_t ev : w.done)
+    if (ev != nullptr) (void)hipEventDestroy(ev);
+  if (w.side != nullptr) {  // (idle: its last work is behind a join the done events cover)
+    (void)hipStreamSynchronize(w.side);
+    (void)hipStreamDestroy(w.side);
+  }
+  for (hipEvent_t ev : {w.fork, w.join})
     if (ev != nullptr) (void)hipEventDestroy(ev);
   if (w.device != cur) (void)hipSetDevice(cur);
   w = Workspace{};
@@ -707,6 +718,19 @@ int RunBatch(DeviceCtx& ctx, const SpanBatch& base_args, bool desc, bool verify,
                       ? 1u
                       : 0u;
   t_last_pair = a.pair_kernel != 0u;
+  // The segment pass (long spans' 32 KiB pieces) needs only the plan: it
+  // runs on the workspace's side stream next to the span kernel, and takes
+  // CUs as the span kernel's groups leave them (~100 us of an SST-descriptor
+  // call ran after it before).  The combine waits for both.
+  if (w->side == nullptr) {
+    e = hipStreamCreateWithFlags(&w->side, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&w->fork, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&w->join, hipEventDisableTiming);
+    if (e != hipSuccess) return FailHip(e, "side stream");
+  }
+  e = hipEventRecord(w->fork, s);
+  if (e == hipSuccess) e = hipStreamWaitEvent(w->side, w->fork, 0);
+  if (e != hipSuccess) return FailHip(e, "side stream fork");
   e = prismdb::dev::launch_span(a, verify, ctx.cus, s);
   if (e != hipSuccess) return FailHip(e, "span kernel launch");
   SpanBatch seg{};
@@ -719,7 +743,9 @@ int RunBatch(DeviceCtx& ctx, const SpanBatch& base_args, bool desc, bool verify,
   seg.role = prismdb::dev::kRoleSegments;
   seg.tabs = ctx.tabs;
   seg.rec = ws.seg_rec;
-  e = prismdb::dev::launch_span(seg, false, ctx.cus, s);
+  e = prismdb::dev::launch_span(seg, false, ctx.cus, w->side);
+  if (e == hipSuccess) e = hipEventRecord(w->join, w->side);
+  if (e == hipSuccess) e = hipStreamWaitEvent(s, w->join, 0);
   if (e != hipSuccess) return FailHip(e, "segment kernel launch");
   e = prismdb::dev::launch_combine(a, desc, verify, ws, s);
   if (e != hipSuccess) return FailHip(e, "combine kernel launch");

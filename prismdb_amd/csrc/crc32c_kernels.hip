@@ -321,6 +321,16 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
   uint32_t res[2] = {0u, 0u}, bad[2] = {0u, 0u};
   uint64_t ta[2] = {0u, 0u};
   const bool seal = (a.flags & kFlagWriteTrailer) != 0;
+  // Priority rotation by SIMD age rank, as in crc32c_pair_kernel: one step
+  // per finished slice.
+  uint32_t prio = rfl(tid >> 6) >> 2;
+  auto set_prio = [&]() {
+    if (prio == 0u) __builtin_amdgcn_s_setprio(0);
+    else if (prio == 1u) __builtin_amdgcn_s_setprio(1);
+    else if (prio == 2u) __builtin_amdgcn_s_setprio(2);
+    else __builtin_amdgcn_s_setprio(3);
+  };
+  set_prio();
   auto flush = [&](int s, const Task& t) {
     const uint32_t base = t.b - t.slot();
     if (lane <= t.slot()) {
@@ -329,6 +339,8 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
       if (seal && ta[s] != 0u) store_le32(reinterpret_cast<const uint8_t*>(ta[s]), res[s]);
     }
     if (seal) ta[s] = 0u;
+    prio = (prio + 1u) & 3u;
+    set_prio();
   };
   // End of a span: tail bytes, conditioning, outputs.
   auto finish = [&](int s, const Task& t, uint32_t e, uint32_t body) {
@@ -512,6 +524,26 @@ __global__ __launch_bounds__(kThreads) void crc32c_pair_kernel(SpanBatch a) {
   const bool masked = (a.flags & kFlagMask) != 0;
   const bool seal = (a.flags & kFlagWriteTrailer) != 0;
 
+  // Priority rotation.  Waves k, k + 4, k + 8, k + 12 of a group share SIMD
+  // k % 4, and at equal user priority the older wave issues first: with equal
+  // runs, a bulk SST batch's waves left at 7.7 / 8.7 / 10.2 / 11.6 ms by age
+  // rank, the youngest alone at the end (tools/wave_timeline.py,
+  // profiles/r05/r05e/r05e_wave_pair_ts.json).  A wave's user priority is
+  // (rank + runs started) mod 4 (s_setprio: user priority ranks ahead of
+  // age), so every wave spends a quarter of its runs at each level: exits
+  // 9.6-10.5 ms, SST descriptors +4.2 %, sealed +4.3 %, 4 KiB descriptors
+  // +4.3 % (r05e_variants_simd_rank_balance.json).  (Static run weights by
+  // rank gained 1.6 %; the fixed kernel, whose remaining waves keep HBM busy
+  // after the oldest leave, gains nothing from either.)
+  uint32_t prio = rfl(tid >> 6) >> 2;
+  auto set_prio = [&]() {
+    if (prio == 0u) __builtin_amdgcn_s_setprio(0);
+    else if (prio == 1u) __builtin_amdgcn_s_setprio(1);
+    else if (prio == 2u) __builtin_amdgcn_s_setprio(2);
+    else __builtin_amdgcn_s_setprio(3);
+  };
+  set_prio();
+
   // Issue-side cursor: run k = [lo, hi) records, pair i of it.
   uint32_t k = wave, lo = 0, hi = 0, i = 0;
   auto run_bounds = [&](uint32_t kk) {
@@ -530,6 +562,8 @@ __global__ __launch_bounds__(kThreads) void crc32c_pair_kernel(SpanBatch a) {
       k += nwaves;
       i = 0;
       if (k < K) run_bounds(k);
+      prio = (prio + 1u) & 3u;
+      set_prio();
     }
   };
   auto read_rec = [&](uint32_t b) -> SpanRec {

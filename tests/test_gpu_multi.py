@@ -156,6 +156,67 @@ def test_multi_failure_hands_streams_back(devices, oracle, native):
     assert len(np.unique(got)) > nb - 64  # every span its own result, not a leftover fill
 
 
+def test_multi_failure_after_second_partition(devices, oracle, native):
+    """With two or more devices: an injected failure right after partition
+    1's batch is enqueued (fail_after = 1) makes every enqueued partition's
+    caller stream wait for the clique's work -- a fill enqueued on each right
+    after the failed call lands after that partition's batch -- and the next
+    call gathers every partition's own results.  (Unverified on a 1-GPU
+    lease: skipped there; the driver's multi-GPU node runs it.)"""
+    import torch
+    from prismdb_amd import crc32c
+    from prismdb_amd._lib import NativeLibraryError
+
+    if len(devices) < 2:
+        pytest.skip("needs two devices")
+    nb = 1 << 17
+    parts, bufs, want = [], [], []
+    for k, d in enumerate(devices[:2]):
+        dev = torch.device("cuda", d)
+        host = oracle.synth(nb * 4096 + 64, 0x5EED0330 + k)
+        off = np.arange(nb, dtype=np.uint64) * 4096
+        lens = np.full(nb, 4096, dtype=np.uint32)
+        parts.append(_to(dev, host, off, lens))
+        want.append(oracle.batch(host[:64 * 4096], off[:64], lens[:64])[0])
+        bufs.append(torch.zeros(16, dtype=torch.int32, device=dev))
+    for d in devices[:2]:
+        torch.cuda.synchronize(d)
+    prev = native.prismdb_crc32c_multi_fail_after(1)
+    try:
+        with pytest.raises(NativeLibraryError, match="injected failure"):
+            crc32c.batch_multi(parts, check_bounds=False)
+        for b in bufs:  # on each device's current stream: after the failed call's work there
+            with torch.cuda.device(b.device):
+                b.fill_(7)
+    finally:
+        native.prismdb_crc32c_multi_fail_after(prev)
+    for d in devices[:2]:
+        torch.cuda.synchronize(d)
+    assert all(bool((b == 7).all()) for b in bufs)
+    out, _ = crc32c.batch_multi(parts, check_bounds=False)
+    got = _u32(out)
+    np.testing.assert_array_equal(got[:64], want[0])
+    np.testing.assert_array_equal(got[nb:nb + 64], want[1])
+
+
+def test_multi_timing_diagnostics(devices, oracle):
+    """prismdb_crc32c_multi_timing: after a batch_multi call, one batch time
+    and one gather time per device of the clique (HIP events on the clique's
+    streams) and the clique's ncclCommInitAll wall time; None for a device
+    list that has no clique."""
+    import torch
+    from prismdb_amd import crc32c
+
+    dev = torch.device("cuda", devices[0])
+    host, off, lens = _partition(oracle, 0x5EED0340, 20000, 0)
+    crc32c.batch_multi([_to(dev, host, off, lens)], mask=True)
+    torch.cuda.synchronize()
+    tm = crc32c.multi_timing([devices[0]])
+    assert tm is not None and len(tm["batch_ms"]) == 1 and len(tm["gather_ms"]) == 1
+    assert tm["batch_ms"][0] > 0.0 and tm["gather_ms"][0] >= 0.0 and tm["init_ms"] > 0.0
+    assert crc32c.multi_timing([devices[0], 63]) is None
+
+
 def test_multi_rejects_bad_outputs(devices):
     """out / mismatch shorter than the partitions' total, of the wrong dtype
     or not on the root device are rejected before the C ABI writes them."""

@@ -248,11 +248,11 @@ VARIANTS = {
                     "        if (seal && ta != 0u) asm volatile(\"global_store_dword %0, %1, off sc0 sc1\" : : \"v\"(ta), \"v\"(res) : \"memory\");\n")],
     # the one-launch kernel's static runs weighted by the wave's place in its
     # group (waves 0-3 / 4-7 / 8-11)
-    "w543": [("crc32c_direct.hip", "constexpr uint32_t kRunWeight[3] = {1u, 1u, 1u};",
+    "w543": [("crc32c_direct.hip", "constexpr uint32_t kRunWeight[3] = {8u, 7u, 6u};",
               "constexpr uint32_t kRunWeight[3] = {5u, 4u, 3u};")],
-    "w654": [("crc32c_direct.hip", "constexpr uint32_t kRunWeight[3] = {1u, 1u, 1u};",
+    "w654": [("crc32c_direct.hip", "constexpr uint32_t kRunWeight[3] = {8u, 7u, 6u};",
               "constexpr uint32_t kRunWeight[3] = {6u, 5u, 4u};")],
-    "w765": [("crc32c_direct.hip", "constexpr uint32_t kRunWeight[3] = {1u, 1u, 1u};",
+    "w765": [("crc32c_direct.hip", "constexpr uint32_t kRunWeight[3] = {8u, 7u, 6u};",
               "constexpr uint32_t kRunWeight[3] = {7u, 6u, 5u};")],
     # the one-launch ring raising the priority of waves with more ring spans
     # left (s_setprio 0-3 by spans not yet started, after every issue)
@@ -292,9 +292,84 @@ VARIANTS["walsafe"] = [
      "        vmeta |= (sec ? 1u : 0u) << 26;\n"
      "      }\n"),
 ]
+# measurement: the pair-run kernel's per-wave entry and exit times
+# (s_memrealtime, 100 MHz) written after the results (tools/wave_timeline.py)
+VARIANTS["pair_ts"] = [
+    ("crc32c_kernels.hip",
+     "  __shared__ uint32_t lds[kLdsWords];\n  const uint32_t tid = threadIdx.x;\n  load_tables(lds, a.tabs, tid);\n"
+     "  __syncthreads();\n  const uint32_t lane = tid & 63u;\n",
+     "  __shared__ uint32_t lds[kLdsWords];\n  const uint32_t tid = threadIdx.x;\n"
+     "  const uint64_t ts0 = __builtin_amdgcn_s_memrealtime();\n  load_tables(lds, a.tabs, tid);\n"
+     "  __syncthreads();\n  const uint32_t lane = tid & 63u;\n"),
+    ("crc32c_kernels.hip",
+     "  // the abandoned slot's loads retire while their registers are live\n#pragma unroll\n"
+     "  for (int sl = 0; sl < 2; ++sl) {\n    wait_task<0>(wb[sl][0], eb[sl][0]);\n"
+     "    wait_task<0>(wb[sl][1], eb[sl][1]);\n  }\n}\n",
+     "  // the abandoned slot's loads retire while their registers are live\n#pragma unroll\n"
+     "  for (int sl = 0; sl < 2; ++sl) {\n    wait_task<0>(wb[sl][0], eb[sl][0]);\n"
+     "    wait_task<0>(wb[sl][1], eb[sl][1]);\n  }\n"
+     "  if (a.out != nullptr && lane < 2u) {\n"
+     "    const uint64_t ts1 = __builtin_amdgcn_s_memrealtime();\n"
+     "    reinterpret_cast<uint64_t*>(a.out + ((n + 3u) & ~3u))[2u * wave + lane] = lane == 0u ? ts0 : ts1;\n"
+     "  }\n}\n"),
+] + MEASURE_ONLY
+# SIMD-slot priority rotation: a wave's user priority (s_setprio) is
+# (its age rank on its SIMD + runs done) mod 4, so over four runs every wave
+# spends a run at every priority (the youngest wave of each SIMD otherwise
+# trails: profiles/r05/r05d_pair_wave_timeline.json)
+SETPRIO = (
+    "          if (rot == 0u) __builtin_amdgcn_s_setprio(0);\n"
+    "          else if (rot == 1u) __builtin_amdgcn_s_setprio(1);\n"
+    "          else if (rot == 2u) __builtin_amdgcn_s_setprio(2);\n"
+    "          else __builtin_amdgcn_s_setprio(3);\n")
+VARIANTS["fixed_rot"] = [
+    ("crc32c_kernels.hip",
+     "  uint64_t cur = wave * kRun;  // first span of the pair being folded\n  if (cur >= n) return;\n",
+     "  uint64_t cur = wave * kRun;  // first span of the pair being folded\n  if (cur >= n) return;\n"
+     "  uint32_t rot = rfl((tid >> 6) >> 2);\n  {\n" + SETPRIO + "  }\n"),
+    ("crc32c_kernels.hip",
+     "        if (nxt >= n || (nxt & (kRun - 1u)) == 0) flush();\n",
+     "        if (nxt >= n || (nxt & (kRun - 1u)) == 0) {\n          flush();\n          rot = (rot + 1u) & 3u;\n"
+     + SETPRIO + "        }\n"),
+]
+# measurement: the fixed kernel's per-wave entry and exit (tools/wave_timeline.py --work fixed)
+VARIANTS["fixed_ts"] = [
+    ("crc32c_kernels.hip",
+     "  const uint64_t n = a.n;\n  __shared__ uint32_t lds[kLdsWords];\n  const uint32_t tid = threadIdx.x;\n",
+     "  const uint64_t n = a.n;\n  __shared__ uint32_t lds[kLdsWords];\n  const uint32_t tid = threadIdx.x;\n"
+     "  const uint64_t ts0 = __builtin_amdgcn_s_memrealtime();\n"),
+    ("crc32c_kernels.hip",
+     "    for (int j = 0; j < K; ++j) asm volatile(\"\" : \"+v\"(ring[d][j]));\n  }\n}\n",
+     "    for (int j = 0; j < K; ++j) asm volatile(\"\" : \"+v\"(ring[d][j]));\n  }\n"
+     "  if (a.out != nullptr && lane < 2u) {\n"
+     "    const uint64_t ts1 = __builtin_amdgcn_s_memrealtime();\n"
+     "    reinterpret_cast<uint64_t*>(a.out + ((n + 3u) & ~3ull))[2u * wave + lane] = lane == 0u ? ts0 : ts1;\n"
+     "  }\n}\n"),
+] + MEASURE_ONLY
+VARIANTS["span_rot"] = [
+    ("crc32c_kernels.hip",
+     "  const ShortShift ss = short_shift_cols(lane);\n  // Per stream:",
+     "  const ShortShift ss = short_shift_cols(lane);\n  uint32_t rot = rfl((tid >> 6) >> 2);\n  {\n" + SETPRIO +
+     "  }\n  // Per stream:"),
+    ("crc32c_kernels.hip",
+     "    else open(c, c.k + kstep, st);\n",
+     "    else {\n      open(c, c.k + kstep, st);\n      rot = (rot + 1u) & 3u;\n" + SETPRIO + "    }\n"),
+]
+# the lane kernel: 8 waves per CU, two per SIMD (ranks 0 and 1)
+VARIANTS["lane_rot"] = [
+    ("crc32c_kernels.hip",
+     "  const uint32_t first = next_run(wave * 64u);\n  if (first >= n) return;\n",
+     "  const uint32_t first = next_run(wave * 64u);\n  if (first >= n) return;\n"
+     "  uint32_t rot = rfl((tid >> 6) >> 2);\n  {\n" + SETPRIO + "  }\n"),
+    ("crc32c_kernels.hip",
+     "      t.nrb = next_run(t.rb + 64u * nwaves);\n",
+     "      t.nrb = next_run(t.rb + 64u * nwaves);\n      rot = (rot + 1u) & 1u;\n" + SETPRIO),
+]
+VARIANTS["rot_span_lane"] = VARIANTS["span_rot"] + VARIANTS["lane_rot"]
+VARIANTS["fixed_ts_rot"] = VARIANTS["fixed_ts"] + VARIANTS["fixed_rot"]
 # combinations
-VARIANTS["w876"] = [("crc32c_direct.hip", "constexpr uint32_t kRunWeight[3] = {1u, 1u, 1u};",
-                     "constexpr uint32_t kRunWeight[3] = {8u, 7u, 6u};")]
+VARIANTS["w111"] = [("crc32c_direct.hip", "constexpr uint32_t kRunWeight[3] = {8u, 7u, 6u};",
+                     "constexpr uint32_t kRunWeight[3] = {1u, 1u, 1u};")]
 VARIANTS["w765prio"] = VARIANTS["w765"] + VARIANTS["prio"]
 VARIANTS["w654prio"] = VARIANTS["w654"] + VARIANTS["prio"]
 VARIANTS["ts_w765"] = VARIANTS["direct_ts"] + VARIANTS["w765"]
