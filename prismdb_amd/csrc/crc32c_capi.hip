@@ -667,10 +667,14 @@ int RunBatch(DeviceCtx& ctx, const SpanBatch& base_args, bool desc, bool verify,
   t_last_direct = false;
   t_last_owned = w->owned;
   t_last_epoch = g_release_epoch.load(std::memory_order_acquire);
-  // Sealing: the lane and span kernels leave the trailers to one pass after
-  // them (crc32c_trailer_kernel), which reads the results back -- from
-  // scratch when the caller passed no `out`.
-  const bool trailer_pass = (a.flags & prismdb::dev::kFlagWriteTrailer) != 0;
+  // Sealing: the span kernels leave the trailers to one pass after them
+  // (crc32c_trailer_kernel), which reads the results back -- from scratch
+  // when the caller passed no `out`.  Not behind the lane kernel: it stores
+  // each log record's header crc as the record finishes, and that measured
+  // 5 % faster on ~1 KB WAL records than the pass (3931 against 3739 GB/s,
+  // profiles/r05/r05g_variants_lane_seal.json) -- a lane's store is one of
+  // 64 records' in flight, not a wave-wide stall.
+  const bool trailer_pass = (a.flags & prismdb::dev::kFlagWriteTrailer) != 0 && !lane;
   if (trailer_pass) {
     a.flags &= ~prismdb::dev::kFlagWriteTrailer;
     if (a.out == nullptr) {

@@ -1217,6 +1217,12 @@ __global__ __launch_bounds__(kLaneThreads) void crc32c_lane_kernel(SpanBatch a) 
   };
   const uint32_t first = next_run(wave * 64u);
   if (first >= n) return;
+  // Priority rotation by SIMD age rank (two waves per SIMD here), as in
+  // crc32c_pair_kernel: one step per run (WAL verify +1.1-1.3 %, seal
+  // +0.8-0.9 %; profiles/r05/r05f_variants_rotation.json, r05g_variants_lane_seal.json).
+  uint32_t prio = rfl(tid >> 6) >> 2;
+  if (prio == 0u) __builtin_amdgcn_s_setprio(0);
+  else __builtin_amdgcn_s_setprio(1);
   const bool hdr = (a.flags & kFlagLogHeader) != 0;
   const bool has_init = a.init != nullptr;
   // lanes without a record of the kernel's read a 2 KiB zero region (per wave)
@@ -1268,6 +1274,9 @@ __global__ __launch_bounds__(kLaneThreads) void crc32c_lane_kernel(SpanBatch a) 
       t.K = K;
       t.kf = kf < K ? kf : K;
       t.nrb = next_run(t.rb + 64u * nwaves);
+      prio ^= 1u;
+      if (prio == 0u) __builtin_amdgcn_s_setprio(0);
+      else __builtin_amdgcn_s_setprio(1);
     }
     // Side loads: the next run's descriptors with a run's first task, the
     // head dword with it, the end dword and the stored crc with its last.

@@ -346,26 +346,27 @@ VARIANTS["fixed_ts"] = [
      "    reinterpret_cast<uint64_t*>(a.out + ((n + 3u) & ~3ull))[2u * wave + lane] = lane == 0u ? ts0 : ts1;\n"
      "  }\n}\n"),
 ] + MEASURE_ONLY
-VARIANTS["span_rot"] = [
+# measurement: the span kernel's per-wave entry and exit (tools/wave_timeline.py --work mixed)
+VARIANTS["span_ts"] = [
     ("crc32c_kernels.hip",
-     "  const ShortShift ss = short_shift_cols(lane);\n  // Per stream:",
-     "  const ShortShift ss = short_shift_cols(lane);\n  uint32_t rot = rfl((tid >> 6) >> 2);\n  {\n" + SETPRIO +
-     "  }\n  // Per stream:"),
+     "  if (blockIdx.x * 2u * kWavesPerGroup >= K) return;\n\n\n  __shared__ uint32_t lds[kLdsWords];\n",
+     "  if (blockIdx.x * 2u * kWavesPerGroup >= K) return;\n"
+     "  const uint64_t ts0 = __builtin_amdgcn_s_memrealtime();\n\n  __shared__ uint32_t lds[kLdsWords];\n"),
     ("crc32c_kernels.hip",
-     "    else open(c, c.k + kstep, st);\n",
-     "    else {\n      open(c, c.k + kstep, st);\n      rot = (rot + 1u) & 3u;\n" + SETPRIO + "    }\n"),
-]
-# the lane kernel: 8 waves per CU, two per SIMD (ranks 0 and 1)
-VARIANTS["lane_rot"] = [
-    ("crc32c_kernels.hip",
-     "  const uint32_t first = next_run(wave * 64u);\n  if (first >= n) return;\n",
-     "  const uint32_t first = next_run(wave * 64u);\n  if (first >= n) return;\n"
-     "  uint32_t rot = rfl((tid >> 6) >> 2);\n  {\n" + SETPRIO + "  }\n"),
-    ("crc32c_kernels.hip",
-     "      t.nrb = next_run(t.rb + 64u * nwaves);\n",
-     "      t.nrb = next_run(t.rb + 64u * nwaves);\n      rot = (rot + 1u) & 1u;\n" + SETPRIO),
-]
-VARIANTS["rot_span_lane"] = VARIANTS["span_rot"] + VARIANTS["lane_rot"]
+     "  // fixed kernel's drain).  Every slice was stored when its last record retired.\n#pragma unroll\n"
+     "  for (int sl = 0; sl < 2; ++sl) {\n    wait_task<0>(wb[sl][0], eb[sl][0]);\n"
+     "    wait_task<0>(wb[sl][1], eb[sl][1]);\n  }\n}\n",
+     "  // fixed kernel's drain).  Every slice was stored when its last record retired.\n#pragma unroll\n"
+     "  for (int sl = 0; sl < 2; ++sl) {\n    wait_task<0>(wb[sl][0], eb[sl][0]);\n"
+     "    wait_task<0>(wb[sl][1], eb[sl][1]);\n  }\n"
+     "  if (a.out != nullptr && a.role == kRoleSpans && a.n_dev == nullptr && lane < 2u) {\n"
+     "    const uint64_t ts1 = __builtin_amdgcn_s_memrealtime();\n"
+     "    reinterpret_cast<uint64_t*>(a.out + ((n + 3u) & ~3u))[2u * wave + lane] = lane == 0u ? ts0 : ts1;\n"
+     "  }\n}\n"),
+] + MEASURE_ONLY
+# the span kernel's task-balanced slices: 32 per stream instead of 16
+VARIANTS["slices32"] = [("crc32c_device.h", "constexpr uint32_t kSlicesPerStream = 16;",
+                         "constexpr uint32_t kSlicesPerStream = 32;")]
 VARIANTS["fixed_ts_rot"] = VARIANTS["fixed_ts"] + VARIANTS["fixed_rot"]
 # combinations
 VARIANTS["w111"] = [("crc32c_direct.hip", "constexpr uint32_t kRunWeight[3] = {8u, 7u, 6u};",

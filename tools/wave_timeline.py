@@ -26,8 +26,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--lib", default=os.path.join(ROOT, "tools", "vlib", "lib_pair_ts.so"))
     ap.add_argument("--spans", type=int, default=1 << 24)
-    ap.add_argument("--work", choices=["sst", "fixed"], default="sst",
-                    help="sst: SST descriptors (pair-run kernel); fixed: 16 Mi x 4 KiB fixed blocks (fixed kernel)")
+    ap.add_argument("--work", choices=["sst", "fixed", "mixed"], default="sst",
+                    help="sst: SST descriptors (pair-run kernel); fixed: 16 Mi x 4 KiB fixed blocks (fixed kernel); "
+                         "mixed: config 3's 1/4/16/64 KiB spans, 32 GiB (span kernel)")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -56,6 +57,11 @@ def main():
     if args.work == "fixed":
         n = args.spans
         off, lens = off[:1], lens[:1]
+    elif args.work == "mixed":
+        rng = np.random.default_rng(0x5EED0003)
+        lens = rng.choice([1024, 4096, 16384, 65536], size=(32 << 30) // 21760).astype(np.int64)
+        off = np.concatenate([[0], np.cumsum(lens)[:-1]])
+        n = len(off)
     buf = torch.empty(max(files * fb, n * 4096) + 64, dtype=torch.uint8, device=dev)
     crc32c.fill_synthetic(buf, 0x5EED0001)
     d_off = torch.from_numpy(off).to(dev)
