@@ -660,7 +660,9 @@ int RunBatch(DeviceCtx& ctx, const SpanBatch& base_args, bool desc, bool verify,
   // its kernels are in git history: crc32c_kernels.hip at 36498f1.)
   const uint32_t streams = 2u * (uint32_t)ctx.cus * prismdb::dev::kWavesPerGroup;
   if ((rc = PlannerWorkspace(*w, s, a.n, streams, lane, &ws)) != 0) return rc;
-  hipError_t e = hipMemsetAsync(ws.counters, 0, sizeof(SplitCounters), s);
+  // (the whole 256-B counter block: one fill kernel; 56 bytes took two)
+  static_assert(sizeof(SplitCounters) <= 256, "the workspace reserves 256 B for the counters");
+  hipError_t e = hipMemsetAsync(ws.counters, 0, 256, s);
   if (e != hipSuccess) return FailHip(e, "hipMemsetAsync");
   t_last_counters = ws.counters;
   t_last_stream = s;
@@ -713,6 +715,7 @@ int RunBatch(DeviceCtx& ctx, const SpanBatch& base_args, bool desc, bool verify,
     if (e != hipSuccess) return FailHip(e, "slice kernels launch");
     a.slice_start = ws.slice_start;
     a.nslices_dev = &ws.counters->nslices;
+    a.tasks_dev = &ws.counters->tasks;
   }
   // Large batches of one-task records take the pair-run kernel (its two
   // streams read adjacent spans); it is launched next to the general one,
@@ -722,6 +725,7 @@ int RunBatch(DeviceCtx& ctx, const SpanBatch& base_args, bool desc, bool verify,
                       ? 1u
                       : 0u;
   t_last_pair = a.pair_kernel != 0u;
+  a.claim = &ws.counters->claim;  // (zeroed with the counters above)
   // The segment pass (long spans' 32 KiB pieces) needs only the plan: it
   // runs on the workspace's side stream next to the span kernel, and takes
   // CUs as the span kernel's groups leave them (~100 us of an SST-descriptor

@@ -100,6 +100,10 @@ struct SpanBatch {
   // Span role: the pair-run span kernel is launched too (it takes the batch
   // when the scan finds every record one task; the general kernel then leaves).
   uint32_t pair_kernel;
+  // nullable, zero at launch: the span kernel's claim counter for its last
+  // kTailRounds rounds of slices or runs (dealt on demand, not statically)
+  uint32_t* claim;
+  const unsigned long long* tasks_dev;  // nullable: the span pass's chunk tasks (slice scan)
 };
 
 // Below this many spans the pair-run kernel's extra launch (~5 us) costs more
@@ -114,6 +118,7 @@ struct SplitCounters {
   unsigned long long nslices;  // task-balanced slices (0: every record one task, runs instead)
   unsigned long long nlist;             // spans the lane kernel leaves to the generic path
   unsigned long long slice_q, slice_r;  // exact slices: q = T / K, r = T % K
+  uint32_t claim;                       // span kernel: tail slices claimed (SpanBatch::claim)
 };
 
 struct SplitWs {

@@ -51,6 +51,14 @@ namespace {
 constexpr int kRing = 4;               // fixed kernel: span buffers in the prefetch ring (even)
 constexpr uint32_t kRunLg = 5;         // fixed kernel: log2(pair steps per run): runs of 64 spans
 constexpr uint32_t kRunsPerStream = 64;  // span kernel: one-task runs shrink until every stream gets this many
+// Rounds of slices / runs claimed on demand at the end of the span kernel
+// (of 16 slices per stream) and the pair-run kernel (of >= 64 runs per wave).
+// Against none, with 10 reps side by side (profiles/r05/r05l_variants_tail_confirm.json,
+// A/A within 0.6 %): config-3 mix +3.4 %, random spans +3.3 %, SST
+// descriptors +3.5 %, sealed +3.0 %, 4 KiB descriptors +2.7 %; 8 / 8 rounds
+// sat between (and cost 4 KiB descriptors 2 %), 2 and 4 ran no faster.
+constexpr uint32_t kTailRounds = 12;
+constexpr uint32_t kPairTailRounds = 16;
 }  // namespace
 }  // namespace dev
 }  // namespace prismdb
@@ -159,9 +167,32 @@ __global__ __launch_bounds__(kThreads) void crc32c_span_kernel(SpanBatch a) {
   struct Cursor {
     uint32_t b, lo, hi, k;
   };
-  // first slice or run >= k of stream st with a record for it
+  // Dynamic tail: slices (runs) k < Kst are dealt statically, k to stream
+  // k mod S; the last kTailRounds rounds go to whichever stream asks first
+  // (one atomic on a per-call counter per slice; its result is waited for
+  // with the ring's loads, once per tail slice).  Waves drain at different
+  // times -- by XCD as well as by SIMD rank, e.g. config 3's exits 4.5-5.6 ms
+  // (profiles/r05/r05e/r05h_wave_span_ts_mixed.json) -- and the early ones
+  // take the tail.
+  // Claims cost an atomic on one address each: the tail shrinks with the
+  // slices (runs) below 32 tasks and is dropped below 16, so the short
+  // slices of a small batch do not turn it into a queue on the counter (2.4 M
+  // SST spans at 4.6 pairs per run: 65 K claims in 1.8 ms ran 20 % slower
+  // than no tail, 8 K claims still 1.3 %; profiles/r05/r05m/r05m_bench.json,
+  // r05n_variants_tail_scaled.json).
+  const uint32_t per = sliced ? (a.tasks_dev != nullptr ? (uint32_t)(const_load(a.tasks_dev, 0) / K) : 32u)
+                              : rq;
+  const uint32_t tail = per >= 32u ? kTailRounds : (per >= 16u ? kTailRounds * per / 32u : 0u);
+  const uint32_t Kst = a.claim != nullptr && K > tail * kstep ? K - tail * kstep : K;
+  // first slice or run >= k of stream st with a record for it (past Kst: claimed)
   auto open = [&](Cursor& c, uint32_t k, uint32_t st) {
-    for (; k < K; k += kstep) {
+    for (; k < K; k = k < Kst ? k + kstep : Kst) {  // (a claimed slice without records: claim again)
+      if (k >= Kst) {
+        uint32_t got = 0;
+        if (lane == 0u) got = __hip_atomic_fetch_add(a.claim, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        k = Kst + rfl(got);
+        if (k >= K) break;
+      }
       uint32_t lo, hi;
       if (sliced) {
         lo = (uint32_t)const_load(a.slice_start, k);
@@ -544,13 +575,23 @@ __global__ __launch_bounds__(kThreads) void crc32c_pair_kernel(SpanBatch a) {
   };
   set_prio();
 
-  // Issue-side cursor: run k = [lo, hi) records, pair i of it.
+  // Issue-side cursor: run k = [lo, hi) records, pair i of it.  Runs past
+  // Kst (the last kTailRounds rounds) are claimed on demand, as in
+  // crc32c_span_kernel (runs are never empty).
+  const uint32_t ptail = rq >= 31u ? kPairTailRounds : (rq >= 16u ? kPairTailRounds * rq / 31u : 0u);  // (the span kernel's note)
+  const uint32_t Kst = a.claim != nullptr && K > ptail * nwaves ? K - ptail * nwaves : K;
+  auto claim_run = [&]() -> uint32_t {
+    uint32_t got = 0;
+    if (lane == 0u) got = __hip_atomic_fetch_add(a.claim, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return Kst + rfl(got);
+  };
   uint32_t k = wave, lo = 0, hi = 0, i = 0;
   auto run_bounds = [&](uint32_t kk) {
     lo = 2u * (kk * rq + (kk < rr ? kk : rr));
     hi = lo + 2u * (rq + (kk < rr ? 1u : 0u));
     hi = hi < n ? hi : n;
   };
+  if (k >= Kst && k < K) k = claim_run();
   if (k < K) run_bounds(k);
   // b: the pair's first record (n: none left)
   auto pair_first = [&]() -> uint32_t { return k < K ? lo + 2u * i : n; };
@@ -561,6 +602,7 @@ __global__ __launch_bounds__(kThreads) void crc32c_pair_kernel(SpanBatch a) {
     } else {
       k += nwaves;
       i = 0;
+      if (k >= Kst && k < K + nwaves) k = claim_run();
       if (k < K) run_bounds(k);
       prio = (prio + 1u) & 3u;
       set_prio();

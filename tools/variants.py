@@ -367,6 +367,11 @@ VARIANTS["span_ts"] = [
 # the span kernel's task-balanced slices: 32 per stream instead of 16
 VARIANTS["slices32"] = [("crc32c_device.h", "constexpr uint32_t kSlicesPerStream = 16;",
                          "constexpr uint32_t kSlicesPerStream = 32;")]
+# the span kernel's dynamic tail: rounds of slices claimed on demand
+VARIANTS["tail0"] = [("crc32c_kernels.hip", "constexpr uint32_t kTailRounds = 12;", "constexpr uint32_t kTailRounds = 0;"),
+                     ("crc32c_kernels.hip", "constexpr uint32_t kPairTailRounds = 16;",
+                      "constexpr uint32_t kPairTailRounds = 0;")]
+VARIANTS["base_aa"] = []
 VARIANTS["fixed_ts_rot"] = VARIANTS["fixed_ts"] + VARIANTS["fixed_rot"]
 # combinations
 VARIANTS["w111"] = [("crc32c_direct.hip", "constexpr uint32_t kRunWeight[3] = {8u, 7u, 6u};",
@@ -521,6 +526,9 @@ def do_run(args, names):
         # the same spans sealed (MASK | WRITE_TRAILER): the planner path's trailer stores
         "sst3988_seal": (lambda n: libs[n][1](buf.data_ptr(), soff.data_ptr(), slen.data_ptr(), None, ns,
                                               sout.data_ptr(), None, 0x3, sp), ns * (3988 + 4 + 12)),
+        # config 5's per-device batch size: 2.4 M SST spans sealed in one call (planner path, short runs)
+        "sst_c5_seal": (lambda n: libs[n][1](buf.data_ptr(), soff.data_ptr(), slen.data_ptr(), None, 2404116,
+                                             sout.data_ptr(), None, 0x3, sp), 2404116 * (3988 + 4 + 12)),
         "huge64m": (lambda n: libs[n][1](buf.data_ptr(), hoff_.data_ptr(), hlen_.data_ptr(), None, nh,
                                          hout.data_ptr(), None, 0, sp), nh * ((64 << 20) - 5 + 16)),
         "adversarial": (lambda n: libs[n][1](buf.data_ptr(), aoff.data_ptr(), alen.data_ptr(), None, len(al),
@@ -575,7 +583,7 @@ def do_run(args, names):
         work = {w: v for w, v in work.items() if w in args.work}
     res = {w: {n: [] for n in names} for w in work}
     agree = {}
-    outs_of = {"wal": wout, "wal_seal": wout, "sst3988": sout, "sst3988_seal": sout, "sst3988_fixed": sout, "huge64m": hout, "one_huge": hout, "file_fixed": fout,
+    outs_of = {"wal": wout, "wal_seal": wout, "sst3988": sout, "sst3988_seal": sout, "sst_c5_seal": sout, "sst3988_fixed": sout, "huge64m": hout, "one_huge": hout, "file_fixed": fout,
                "file_desc": fout, "file_seal": fout, "files7_seal": f7out, "files7_verify": f7out, "files2_seal": f7out,
                "files2_verify": f7out, "files3_seal": f7out, "files3_verify": f7out,
                "file_verify": fout, "tiny_desc": fout}
