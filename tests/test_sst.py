@@ -82,6 +82,34 @@ def test_seal_blocks_reproduces_reference_trailers(native, golden):
 
 
 @pytest.mark.gpu
+def test_host_seal_reproduces_reference_sst(native, golden):
+    """The reference SST as an output file still in host memory (its append
+    buffer): every trailer zeroed, the block spans listed by the host walker
+    (leveldb_sst_block_spans), all blocks sealed by ONE
+    leveldb_crc32c_batch_host call with MASK | WRITE_TRAILER: byte-identical
+    to what TableBuilder wrote (table/table_builder.cc:185-202), pageable and
+    pinned."""
+    import torch
+    from prismdb_amd import crc32c, sst
+
+    ref = golden["sst_bytes"]
+    off, ln, _ = sst.block_spans(ref)  # contents || type of every block
+    order = np.argsort(off, kind="stable")
+    off, ln = off[order], ln[order]
+    want = {b["offset"]: b["masked_crc"] for b in golden["sst"]["blocks"]}
+    assert set(want) <= set(int(o) for o in off)
+    for pinned in (False, True):
+        f = np.frombuffer(ref, dtype=np.uint8).copy()
+        for o, n in zip(off, ln):
+            f[int(o) + int(n):int(o) + int(n) + 4] = 0
+        host = torch.from_numpy(f).pin_memory() if pinned else f
+        crc, _ = crc32c.batch_host(host, off, ln, mask=True, trailer=True)
+        got = host.numpy() if pinned else host
+        assert got.tobytes() == ref, pinned
+        assert {int(o): int(c) for o, c in zip(off, crc) if int(o) in want} == want
+
+
+@pytest.mark.gpu
 def test_seal_long_block_split_path(native, oracle):
     """Trailer written by the combine kernel for a span above the split threshold."""
     import torch
