@@ -1178,8 +1178,15 @@ __global__ __launch_bounds__(256) void crc32c_combine_kernel(SpanBatch a, SplitW
 //
 // A task is one 128-B line of every lane's record, issued one task ahead into
 // a two-slot ring and retired by counted vmcnt waits.  Task 0 (where bodies
-// start) and tasks past the run's shortest record fold under per-word masks,
-// the others unmasked; a lane past its record re-reads its last line.
+// start) and the lines where some lane's record ends fold under per-word
+// masks; the other lines ("clean": for each lane all body words or past its
+// record) fold unmasked, with one per-lane select.  (The bound used to be the
+// run's shortest record: a log split at a 32 KiB block boundary leaves a
+// short fragment in most runs of 64 records, and with it every later task
+// masked.)  A lane past its record re-reads its last line.  The fold is not
+// what bounds the kernel: clean lines XORed instead of folded (a
+// measurement-only variant) ran no faster, nor did them folded as two or four
+// independent chains per lane (profiles/r05/r05q_variants_lane_chains.json).
 //
 // Load order inside an issue: the next run's descriptors (first task of a
 // run), the edge dwords (first / last task), then the eight body loads, so
@@ -1225,20 +1232,37 @@ __device__ __forceinline__ void wait_lane(u32x4 (&w)[8], uint32_t& hd, uint32_t&
                : "memory");
 }
 
-// Wave-uniform task: run of records [rb, rb + 64), its 128-B task k of K, the
-// first kf unmasked; nrb: the wave's next owned run.
+// Wave-uniform task: run of records [rb, rb + 64), its 128-B task k of K;
+// bit k of pm: some lane's record ends inside line k (a masked task); nrb:
+// the wave's next owned run.
 struct LaneTask {
-  uint32_t rb, k, kf, K, nrb;
+  uint32_t rb, k, pm, K, nrb;
 };
 
-template <int kOp>  // 0: max, 1: min
+template <int kOp>  // 0: max, 1: min, 2: or
 __device__ __forceinline__ uint32_t wave_reduce(uint32_t v) {
-  auto f = [](uint32_t x, uint32_t y) { return kOp == 0 ? (x > y ? x : y) : (x < y ? x : y); };
+  auto f = [](uint32_t x, uint32_t y) { return kOp == 0 ? (x > y ? x : y) : kOp == 1 ? (x < y ? x : y) : (x | y); };
   v = f(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false));  // quad_perm 1,0,3,2
   v = f(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false));  // quad_perm 2,3,0,1
   v = f(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false)); // row_half_mirror
   v = f(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false)); // row_mirror
   return f(f(readlane(v, 0), readlane(v, 16)), f(readlane(v, 32), readlane(v, 48)));
+}
+
+// Word idx (0..31, per lane) of a line in this lane's registers: a five-level
+// select tree (31 v_cndmask).
+__device__ __forceinline__ uint32_t pick_word(const u32x4 (&w)[8], uint32_t idx) {
+  uint32_t v[16];
+  const bool b0 = (idx & 1u) != 0u;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) v[i] = b0 ? w[(2 * i + 1) >> 2][(2 * i + 1) & 3] : w[(2 * i) >> 2][(2 * i) & 3];
+#pragma unroll
+  for (int l = 1; l < 5; ++l) {
+    const bool b = ((idx >> l) & 1u) != 0u;
+#pragma unroll
+    for (int i = 0; i < (16 >> l); ++i) v[i] = b ? v[2 * i + 1] : v[2 * i];
+  }
+  return v[0];
 }
 
 template <bool kVerify>
@@ -1311,10 +1335,10 @@ __global__ __launch_bounds__(kLaneThreads) void crc32c_lane_kernel(SpanBatch a) 
       vkend = owned ? (qe + 31u) >> 5 : 1u;
       vinit = ninit;
       vmeta = n4 | (q0 << 16) | (h << 21) | (tb << 23) | ((owned ? 1u : 0u) << 25);
-      uint32_t K = wave_reduce<0>(vkend);
-      uint32_t kf = wave_reduce<1>(owned ? qe >> 5 : 0xFFFFu);
-      t.K = K;
-      t.kf = kf < K ? kf : K;
+      t.K = wave_reduce<0>(vkend);
+      // the lines holding a record's last body word short of the line's end
+      // (a record ending exactly at a line's end has no such line)
+      t.pm = wave_reduce<2>(owned && (qe & 31u) != 0u ? 1u << (qe >> 5) : 0u);
       t.nrb = next_run(t.rb + 64u * nwaves);
       prio ^= 1u;
       if (prio == 0u) __builtin_amdgcn_s_setprio(0);
@@ -1329,18 +1353,31 @@ __global__ __launch_bounds__(kLaneThreads) void crc32c_lane_kernel(SpanBatch a) 
     // at 16 waves hipcc, short of VGPRs, copied such registers at the merge
     // before their wait; the CFG audit run by build() fails on any such touch,
     // and this build has none.
+    //
+    // A lane reads a side dword from memory only when the line it is in is
+    // not the one the task loads (see fold: the head dword precedes a body
+    // that starts a line, a log header's crc lies in the line before, the
+    // tail bytes follow a body that ends a line); every other lane's address
+    // is the wave's zero region -- one line for the whole instruction instead
+    // of 64 (WAL verify +2.1 %, profiles/r05/r05s_variants_lane_side_dwords.json;
+    // without the side loads at all it would gain 6.6 %: r05r_variants_lane_diagnosis.json).
     constexpr bool kSideAlways = !kVerify;
     const bool live = t.rb < n;
     const bool owned = live && ((vmeta >> 25) & 1u);
     const bool lastk = t.k + 1u == t.K;
+    const uint32_t vq0 = (vmeta >> 16) & 31u, vh = (vmeta >> 21) & 3u, vtb = (vmeta >> 23) & 3u;
+    const uint32_t vqe = vq0 + (vmeta & 0xFFFFu);
     if (kSideAlways || t.k == 0) fetch_desc(t.nrb);
     VP[sl] = vp;
     META[sl] = live ? vmeta : 0u;
     INIT[sl] = vinit;
-    if (kSideAlways || t.k == 0) HD[sl] = asm_load_u32(owned && t.k == 0 ? vp & ~3ull : zero);
+    if (kSideAlways || t.k == 0) {
+      HD[sl] = asm_load_u32(owned && t.k == 0 && vq0 == 0u && vh != 0u ? vp & ~3ull : zero);
+      if (kVerify && hdr) SC[sl] = asm_load_u32(owned && t.k == 0 && 4u * vq0 < vh + kLogCrcBack ? vp - kLogCrcBack : zero);
+    }
     if (kSideAlways || lastk) {
-      ED[sl] = asm_load_u32(owned && lastk ? vp + vlen - 4u : zero);
-      if (kVerify) SC[sl] = asm_load_u32(owned && lastk ? (hdr ? vp - kLogCrcBack : vp + vlen) : zero);
+      ED[sl] = asm_load_u32(owned && lastk && vtb != 0u && (vqe & 31u) == 0u ? vp + vlen - 4u : zero);
+      if (kVerify && !hdr) SC[sl] = asm_load_u32(owned && lastk ? vp + vlen : zero);
     }
     // line min(k, kend - 1) of the lane's record (a finished lane re-reads its last)
     const uint32_t kl = live ? (t.k < vkend ? t.k : vkend - 1u) : 0u;
@@ -1355,12 +1392,13 @@ __global__ __launch_bounds__(kLaneThreads) void crc32c_lane_kernel(SpanBatch a) 
       u.rb = t.nrb;
       u.k = 0;
       u.K = 1;
-      u.kf = 0;
+      u.pm = 0;
     }
     return u;
   };
 
   uint32_t acc = 0;
+  uint32_t hsc = 0;  // a log record's stored crc (its header's), taken at task 0
   auto fold = [&](const LaneTask& t, int sl) {
     const u32x4(&w)[8] = W[sl];
     const uint32_t meta = META[sl];
@@ -1375,7 +1413,16 @@ __global__ __launch_bounds__(kLaneThreads) void crc32c_lane_kernel(SpanBatch a) 
       // the head bytes, then the body from word q0 of the line: the register
       // enters with body word 0
       const uint32_t h = (meta >> 21) & 3u;
-      const uint32_t hb = HD[sl] >> (8u * ((4u - h) & 3u));  // the record's first bytes
+      // the dword before the body (word q0 - 1 of this line, or loaded)
+      const uint32_t hd = q0 != 0u ? pick_word(w, q0 - 1u) : HD[sl];
+      const uint32_t hb = hd >> (8u * ((4u - h) & 3u));  // the record's first bytes
+      if (kVerify && hdr) {
+        // the header's crc: bytes [o, o + 4) of this line, o = 4 q0 - h - 6
+        // (or loaded when o < 0)
+        const uint32_t o = 4u * q0 - h - kLogCrcBack, j = o >> 2;
+        const uint32_t lo = pick_word(w, j & 31u), hi = pick_word(w, j + 1u < 32u ? j + 1u : 31u);
+        hsc = 4u * q0 < h + kLogCrcBack ? SC[sl] : __builtin_amdgcn_alignbyte(hi, lo, o & 3u);
+      }
       uint32_t r = INIT[sl] ^ kConditioning;
 #pragma unroll
       for (uint32_t i = 0; i < 3; ++i) {
@@ -1388,9 +1435,14 @@ __global__ __launch_bounds__(kLaneThreads) void crc32c_lane_kernel(SpanBatch a) 
         const uint32_t y = rel == 0u ? r ^ w[i >> 2][i & 3] : step256(lds, tab, x, w[i >> 2][i & 3]);
         x = rel < n4 ? y : x;
       }
-    } else if (t.k < t.kf) {
+    } else if (((t.pm >> t.k) & 1u) == 0u) {
+      // No record ends inside this line: every lane's line is all body words
+      // (32k + 32 <= q0 + n4), or lies past the lane's record, which keeps
+      // its register.
+      uint32_t y = x;
 #pragma unroll
-      for (int i = 0; i < 32; ++i) x = step256(lds, tab, x, w[i >> 2][i & 3]);
+      for (int i = 0; i < 32; ++i) y = step256(lds, tab, y, w[i >> 2][i & 3]);
+      x = 32u * t.k + 32u <= q0 + n4 ? y : x;
     } else {
       const uint32_t rel0 = 32u * t.k - q0;  // body word index of the line's word 0
 #pragma unroll
@@ -1403,7 +1455,12 @@ __global__ __launch_bounds__(kLaneThreads) void crc32c_lane_kernel(SpanBatch a) 
     if (t.k + 1u == t.K) {
       uint32_t r = step256(lds, tab, x, 0u);  // shift_4 after the last body word
       const uint32_t tb = (meta >> 23) & 3u;
-      const uint32_t fb = tb ? ED[sl] >> (8u * (4u - tb)) : 0u;  // the record's last tb bytes
+      // the record's last tb bytes: the low bytes of word q0 + n4 of this
+      // line (the lane's last), or the top bytes of the loaded end dword when
+      // the body ends the line
+      const uint32_t qe = q0 + n4;
+      const uint32_t fw = (qe & 31u) != 0u ? pick_word(w, qe & 31u) : ED[sl] >> (8u * ((4u - tb) & 3u));
+      const uint32_t fb = tb ? fw & ((1u << (8u * tb)) - 1u) : 0u;
 #pragma unroll
       for (uint32_t i = 0; i < 3; ++i) {
         const uint32_t v = byte_step(r, (fb >> (8u * i)) & 255u);
@@ -1422,13 +1479,13 @@ __global__ __launch_bounds__(kLaneThreads) void crc32c_lane_kernel(SpanBatch a) 
         }
         if (a.out != nullptr) __builtin_nontemporal_store(v, a.out + rec);
         if (kVerify && a.mismatch != nullptr)
-          __builtin_nontemporal_store((uint8_t)(crc != unmask_crc(SC[sl]) ? 1u : 0u), a.mismatch + rec);
+          __builtin_nontemporal_store((uint8_t)(crc != unmask_crc(hdr ? hsc : SC[sl]) ? 1u : 0u), a.mismatch + rec);
       }
     }
   };
 
   LaneTask tk[2];
-  tk[0] = LaneTask{first, 0u, 0u, 1u, n};
+  tk[0] = LaneTask{first, 0u, 0u, 1u, n};  // (pm of a first task: unused)
   issue(tk[0], 0);
   // the next run's descriptors (issued before the eight body loads) may be
   // read by the second issue: retire everything but those eight loads

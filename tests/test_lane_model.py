@@ -5,15 +5,18 @@ For random runs of 64 records (lengths around the kernel's limits, any
 alignment, records the kernel leaves to the generic path among them) the model
 mirrors issue() step by step -- head bytes h, body words n4, tail bytes tb,
 the body's first line vl and first word q0, the lane's last task kend, the
-run's K and unmasked bound kf, the line a lane reads in task k -- and checks:
+run's K and partial-line mask pm, the line a lane reads in task k -- and checks:
 
   * every body load is one whole 128-B line holding a byte of the lane's own
     record (a line with a record byte lies in a mapped page: no fault), and
     the head / end dwords lie inside the record's first / last 4-B word;
   * folding the loaded words with the kernel's masks (task 0: the register
-    enters at word q0; unmasked tasks 1 <= k < kf; masked tasks after) and the
-    edge bytes gives the oracle's crc (oracle/crc32c_oracle.c, pinned to the
-    reference's golden vectors).
+    enters at word q0; tasks whose bit is clear in pm fold unmasked, kept
+    only by lanes whose line is all body; tasks with the bit set fold masked
+    word by word) and the edge bytes -- the head dword, a log header's crc and
+    the tail bytes taken from the line registers where the line holds them,
+    loaded otherwise -- gives the oracle's crc (oracle/crc32c_oracle.c, pinned
+    to the reference's golden vectors).
 
 CPU only: no device is touched."""
 import numpy as np
@@ -60,8 +63,10 @@ def lane_run(buf, offs, lens, inits):
         lanes.append(dict(p=p, ln=ln, owned=owned, h=h, n4=n4, tb=tb, vl=vb & ~127, q0=q0,
                           kend=(qe + 31) >> 5 if owned else 1, qe=qe))
     K = max(x["kend"] for x in lanes)
-    kf = min([x["qe"] >> 5 for x in lanes if x["owned"]] or [0xFFFF])
-    kf = min(kf, K)
+    pm = 0
+    for x in lanes:
+        if x["owned"] and x["qe"] & 31:
+            pm |= 1 << (x["qe"] >> 5)
     acc = [0] * nl
     out = {}
     for k in range(K):
@@ -77,7 +82,18 @@ def lane_run(buf, offs, lens, inits):
                 hd_addr = x["p"] & ~3
                 if not (hd_addr <= x["p"] < hd_addr + 4):
                     bad.append(("head", l))
-                hb = u32(hd_addr) >> (8 * ((4 - x["h"]) & 3))
+                # the head dword from the line (word q0 - 1), loaded only when the body starts the line
+                hd = w[x["q0"] - 1] if x["q0"] else u32(hd_addr)
+                if x["h"] and hd != u32(hd_addr):
+                    bad.append(("head_pick", l))
+                hb = hd >> (8 * ((4 - x["h"]) & 3))
+                # a log header's crc (6 B before the span) from the line, loaded when it starts before it
+                o = 4 * x["q0"] - x["h"] - 6
+                if o >= 0 and x["p"] >= 6:
+                    j, sh = o >> 2, o & 3
+                    pair = w[j] | (w[min(j + 1, 31)] << 32)
+                    if (pair >> (8 * sh)) & 0xFFFFFFFF != u32(x["p"] - 6):
+                        bad.append(("crc_pick", l))
                 r = inits[l] ^ 0xFFFFFFFF
                 for i in range(3):
                     v = byte_step(r, (hb >> (8 * i)) & 255)
@@ -86,9 +102,14 @@ def lane_run(buf, offs, lens, inits):
                     rel = (i - x["q0"]) & 0xFFFFFFFF
                     y = r ^ w[i] if rel == 0 else step(a, w[i])
                     a = y if rel < x["n4"] else a
-            elif k < kf:
+            elif not (pm >> k) & 1:
+                y = a
                 for i in range(32):
-                    a = step(a, w[i])
+                    y = step(y, w[i])
+                if 32 * k + 32 <= x["qe"]:
+                    a = y
+                elif 32 * k < x["qe"]:
+                    bad.append(("clean", l, k))  # a partial line outside pm
             else:
                 rel0 = (32 * k - x["q0"]) & 0xFFFFFFFF
                 for i in range(32):
@@ -100,7 +121,11 @@ def lane_run(buf, offs, lens, inits):
                 ed_addr = x["p"] + x["ln"] - 4
                 if ed_addr < x["p"]:
                     bad.append(("end", l))
-                fb = u32(ed_addr) >> (8 * (4 - x["tb"])) if x["tb"] else 0
+                qe = x["qe"]
+                fw = w[qe & 31] if qe & 31 else u32(ed_addr) >> (8 * ((4 - x["tb"]) & 3))
+                fb = fw & ((1 << (8 * x["tb"])) - 1)
+                if x["tb"] and fb != u32(ed_addr) >> (8 * (4 - x["tb"])):
+                    bad.append(("tail_pick", l))
                 for i in range(3):
                     v = byte_step(r, (fb >> (8 * i)) & 255)
                     r = v if i < x["tb"] else r

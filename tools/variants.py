@@ -372,7 +372,29 @@ VARIANTS["tail0"] = [("crc32c_kernels.hip", "constexpr uint32_t kTailRounds = 12
                      ("crc32c_kernels.hip", "constexpr uint32_t kPairTailRounds = 16;",
                       "constexpr uint32_t kPairTailRounds = 0;")]
 VARIANTS["base_aa"] = []
+# measurement-only (wrong results): what the lane kernel's fold costs on its
+# clean lines -- words XORed instead of folded (no LDS lookups)
+VARIANTS["lane_nofold"] = [("crc32c_kernels.hip", "      for (int i = 0; i < 32; ++i) y = step256(lds, tab, y, w[i >> 2][i & 3]);\n",
+                            "      for (int i = 0; i < 32; ++i) y ^= w[i >> 2][i & 3];\n")] + MEASURE_ONLY
 VARIANTS["fixed_ts_rot"] = VARIANTS["fixed_ts"] + VARIANTS["fixed_rot"]
+# measurement-only (wrong results): the lane kernel's side loads with every
+# lane reading the wave's zero region -- what the remaining ones cost
+VARIANTS["lane_sidezero"] = [
+    ("crc32c_kernels.hip", "      HD[sl] = asm_load_u32(owned && t.k == 0 && vq0 == 0u && vh != 0u ? vp & ~3ull : zero);\n",
+     "      HD[sl] = asm_load_u32(zero);\n"),
+    ("crc32c_kernels.hip",
+     "      if (kVerify && hdr) SC[sl] = asm_load_u32(owned && t.k == 0 && 4u * vq0 < vh + kLogCrcBack ? vp - kLogCrcBack : zero);\n",
+     "      if (kVerify && hdr) SC[sl] = asm_load_u32(zero);\n"),
+    ("crc32c_kernels.hip",
+     "      ED[sl] = asm_load_u32(owned && lastk && vtb != 0u && (vqe & 31u) == 0u ? vp + vlen - 4u : zero);\n",
+     "      ED[sl] = asm_load_u32(zero);\n")] + MEASURE_ONLY
+VARIANTS["lane_noout"] =[("crc32c_kernels.hip", "        if (a.out != nullptr) __builtin_nontemporal_store(v, a.out + rec);\n",
+                           "")] + MEASURE_ONLY
+# the lane kernel at 12 / 16 waves per CU
+VARIANTS["lane_w12"] = [("crc32c_kernels.hip", "constexpr uint32_t kLaneThreads = 512;", "constexpr uint32_t kLaneThreads = 768;")]
+VARIANTS["lane_w16"] = [("crc32c_kernels.hip", "constexpr uint32_t kLaneThreads = 512;", "constexpr uint32_t kLaneThreads = 1024;")]
+# the lane kernel before the partial-line mask (round 5's committed kernels)
+VARIANTS["lane_r05"] = [("crc32c_kernels.hip", "@git", "7af4fee:prismdb_amd/csrc/crc32c_kernels.hip")]
 # combinations
 VARIANTS["w111"] = [("crc32c_direct.hip", "constexpr uint32_t kRunWeight[3] = {8u, 7u, 6u};",
                      "constexpr uint32_t kRunWeight[3] = {1u, 1u, 1u};")]
