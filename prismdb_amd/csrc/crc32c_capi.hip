@@ -479,13 +479,12 @@ int PlannerWorkspace(Workspace& w, hipStream_t s, size_t nspans, uint32_t stream
   if (lane && w.cap_q < nspans) {
     const size_t cap = nspans < 4096 ? 4096 : nspans + nspans / 4;
     w.cap_q = 0;
-    if (int rc = GrowBlock(&w.qgrow, cap * 9 + cap / 64 + 1024, s, "lane list workspace")) return rc;
+    if (int rc = GrowBlock(&w.qgrow, cap * 9 + 1024, s, "lane list workspace")) return rc;
     w.cap_q = cap;
   }
   w.ws.list = lane ? reinterpret_cast<uint32_t*>(w.qgrow) : nullptr;
   w.ws.qout = lane ? reinterpret_cast<uint32_t*>(w.qgrow + w.cap_q * 4) : nullptr;
   w.ws.qmm = lane ? reinterpret_cast<uint8_t*>(w.qgrow + w.cap_q * 8) : nullptr;
-  w.ws.qrun = lane ? reinterpret_cast<uint8_t*>(w.qgrow + w.cap_q * 9) : nullptr;
   w.ws.rec = reinterpret_cast<prismdb::dev::SpanRec*>(w.grow);
   w.ws.slice_start = reinterpret_cast<uint64_t*>(w.grow + w.cap_rec * 16);
   w.ws.cnt = reinterpret_cast<uint32_t*>(w.grow + w.cap_rec * 16 + SliceCap(w.cap_rec, w.cap_streams) * 8);
@@ -575,6 +574,15 @@ int RunWindows(DeviceCtx& ctx, const SpanBatch& a, bool verify, hipStream_t s, u
 // rest: plan (span records, long spans cut into segments) -> span pass (long
 // spans skipped) -> segment pass -> combine, with the lane kernel and its
 // list in front for log-record batches.
+// The workspace's side stream and its fork / join events, created on first use.
+int SideStream(Workspace* w) {
+  if (w->side != nullptr) return 0;
+  hipError_t e = hipStreamCreateWithFlags(&w->side, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&w->fork, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&w->join, hipEventDisableTiming);
+  return e == hipSuccess ? 0 : FailHip(e, "side stream");
+}
+
 int RunBatch(DeviceCtx& ctx, const SpanBatch& base_args, bool desc, bool verify, hipStream_t s, int route) {
   SpanBatch a = base_args;
   // PRISMDB_CRC32C_UNORDERED is accepted and has no effect: every launch is
@@ -692,8 +700,17 @@ int RunBatch(DeviceCtx& ctx, const SpanBatch& base_args, bool desc, bool verify,
   uint32_t* const res_out = a.out;  // the caller's out, or the trailer pass's scratch
   uint8_t* const caller_mm = a.mismatch;
   if (lane) {
-    a.qrun = ws.qrun;
-    e = prismdb::dev::launch_lane(a, verify, ctx.cus, ws, s);
+    // The list of the spans the lane kernel does not own is built on the
+    // side stream while the lane kernel runs; the generic path below waits
+    // for it.
+    if ((rc = SideStream(w)) != 0) return rc;
+    e = hipEventRecord(w->fork, s);
+    if (e == hipSuccess) e = hipStreamWaitEvent(w->side, w->fork, 0);
+    if (e == hipSuccess) e = prismdb::dev::launch_long_list(a, ws, w->side);
+    if (e == hipSuccess) e = hipEventRecord(w->join, w->side);
+    if (e != hipSuccess) return FailHip(e, "long-span list launch");
+    e = prismdb::dev::launch_lane(a, verify, ctx.cus, s);
+    if (e == hipSuccess) e = hipStreamWaitEvent(s, w->join, 0);
     if (e != hipSuccess) return FailHip(e, "lane kernel launch");
     a.idx = ws.list;
     a.n_dev = &ws.counters->nlist;
@@ -730,12 +747,7 @@ int RunBatch(DeviceCtx& ctx, const SpanBatch& base_args, bool desc, bool verify,
   // runs on the workspace's side stream next to the span kernel, and takes
   // CUs as the span kernel's groups leave them (~100 us of an SST-descriptor
   // call ran after it before).  The combine waits for both.
-  if (w->side == nullptr) {
-    e = hipStreamCreateWithFlags(&w->side, hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&w->fork, hipEventDisableTiming);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&w->join, hipEventDisableTiming);
-    if (e != hipSuccess) return FailHip(e, "side stream");
-  }
+  if ((rc = SideStream(w)) != 0) return rc;
   e = hipEventRecord(w->fork, s);
   if (e == hipSuccess) e = hipStreamWaitEvent(w->side, w->fork, 0);
   if (e != hipSuccess) return FailHip(e, "side stream fork");

@@ -96,7 +96,6 @@ struct SpanBatch {
   // descriptors and results (the generic path behind the lane kernel runs
   // over the list of spans it does not own; n_dev holds the list length)
   const uint32_t* idx;
-  const uint8_t* qrun;  // lane kernel: runs it owns a span of (crc32c_long_list_kernel)
   // Span role: the pair-run span kernel is launched too (it takes the batch
   // when the scan finds every record one task; the general kernel then leaves).
   uint32_t pair_kernel;
@@ -141,8 +140,6 @@ struct SplitWs {
   uint32_t* list;         // lane path: indices of the spans the lane kernel does not own
   uint32_t* qout;         // lane path: generic-path results of the listed spans (list order)
   uint8_t* qmm;
-  uint8_t* qrun;          // lane path: per run of 64 spans, 1 if the lane kernel owns one of them
-                          // (read a dword at a time: the workspace has slack around it)
 };
 
 // One-launch path for descriptor batches of <= kDirectMaxSpans spans
@@ -187,7 +184,8 @@ hipError_t launch_plan(const SpanBatch& a, bool desc, const SplitWs& ws, hipStre
 hipError_t launch_slices(const SpanBatch& a, const SplitWs& ws, hipStream_t s);
 hipError_t launch_combine(const SpanBatch& a, bool desc, bool verify, const SplitWs& ws,
                           hipStream_t s);
-hipError_t launch_lane(const SpanBatch& a, bool verify, int grid, const SplitWs& ws, hipStream_t s);
+hipError_t launch_long_list(const SpanBatch& a, const SplitWs& ws, hipStream_t s);
+hipError_t launch_lane(const SpanBatch& a, bool verify, int grid, hipStream_t s);
 constexpr int kListThreads = 1024;  // crc32c_long_list_kernel block: one atomic per 16 runs
 // `done` is recorded when the kernel completes (the launch's own completion
 // signal: a separate hipEventRecord marker cost ~5.7 us between back-to-back

@@ -932,6 +932,10 @@ template <bool kDesc>
 __global__ __launch_bounds__(kPlanThreads) void crc32c_plan_kernel(SpanBatch a, SplitWs ws) {
   const uint64_t n = batch_n(a);
   const uint64_t lo = (uint64_t)blockIdx.x * ws.tile;
+  if (lo >= n) {  // (behind the lane kernel the list is often empty: ~4000 blocks leave at once)
+    if (threadIdx.x == 0) ws.bsum[blockIdx.x] = 0;
+    return;
+  }
   const uint64_t hi = lo + ws.tile < n ? lo + ws.tile : n;
   __shared__ unsigned long long sum;
   if (threadIdx.x == 0) sum = 0;
@@ -1276,11 +1280,11 @@ __global__ __launch_bounds__(kLaneThreads) void crc32c_lane_kernel(SpanBatch a) 
   const StrideLanes tab = stride_lanes(lane);
   const uint32_t wave = rfl(blockIdx.x * (kLaneThreads / 64u) + (tid >> 6));
   const uint32_t nwaves = gridDim.x * (kLaneThreads / 64u);
-  const uint8_t* const qrun = a.qrun;
-  auto next_run = [&](uint32_t rb) -> uint32_t {  // first owned run at or after rb
-    while (rb < n && const_byte(qrun, (uint64_t)(rb >> 6)) == 0u) rb += 64u * nwaves;
-    return rb;
-  };
+  // Every run of the batch: one whose spans the kernel owns none of costs
+  // one task of loads from the zero region.  (Runs used to be skipped by a
+  // flag from crc32c_long_list_kernel, which then had to finish first; it
+  // now runs next to this kernel.)
+  auto next_run = [&](uint32_t rb) -> uint32_t { return rb; };
   const uint32_t first = next_run(wave * 64u);
   if (first >= n) return;
   // Priority rotation by SIMD age rank (two waves per SIMD here), as in
@@ -1516,9 +1520,10 @@ drained:
 // The spans the lane kernel leaves to the generic path (lane_owns() false),
 // listed run by run (a wave's 64 consecutive spans stay together and in
 // order); ws.counters->nlist is the count.  One atomic per block of 16 runs
-// (one per run serialized on the counter: 790 us for 64 Ki runs).
-// ws.qrun[r] = 1 if the lane kernel owns a span of run r: it skips the other
-// runs.
+// (one per run serialized on the counter: 790 us for 64 Ki runs).  Launched
+// on a side stream next to the lane kernel (it reads ~12 B per span, ~60 us
+// of a 17 M-record WAL batch that used to sit in front of the lane kernel:
+// WAL verify +2.7 %, seal +1.4 %, profiles/r05/r05v_variants_lane_side_list.json).
 __global__ __launch_bounds__(kListThreads) void crc32c_long_list_kernel(SpanBatch a, SplitWs ws) {
   const uint64_t n = a.n;
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
@@ -1531,11 +1536,7 @@ __global__ __launch_bounds__(kListThreads) void crc32c_long_list_kernel(SpanBatc
     const bool mine = i < n && lane_owns(a.len[i < n ? i : n - 1u]);
     const bool lng = i < n && !mine;
     const uint64_t m = __ballot(lng);
-    const uint64_t own = __ballot(mine);
-    if (lane == 0) {
-      cnt[wv] = (uint32_t)__popcll(m);
-      if (i < n) ws.qrun[i >> 6] = own ? 1u : 0u;
-    }
+    if (lane == 0) cnt[wv] = (uint32_t)__popcll(m);
     __syncthreads();
     if (threadIdx.x == 0) {
       uint32_t tot = 0;
@@ -1638,13 +1639,17 @@ hipError_t launch_slices(const SpanBatch& a, const SplitWs& ws, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_lane(const SpanBatch& a, bool verify, int grid, const SplitWs& ws, hipStream_t s) {
+hipError_t launch_long_list(const SpanBatch& a, const SplitWs& ws, hipStream_t s) {
   const uint64_t lb = (a.n + kListThreads - 1) / kListThreads;
   // one block per 1024 spans up to 16 Mi spans (a grid of 1024 looped and
   // took 49 us over a 4 GiB WAL batch; the atomics are per block-iteration
   // either way)
   const int lgrid = (int)(lb < 16384u ? lb : 16384u);
   crc32c_long_list_kernel<<<lgrid, kListThreads, 0, s>>>(a, ws);
+  return hipGetLastError();
+}
+
+hipError_t launch_lane(const SpanBatch& a, bool verify, int grid, hipStream_t s) {
   if (verify) crc32c_lane_kernel<true><<<grid, kLaneThreads, 0, s>>>(a);
   else crc32c_lane_kernel<false><<<grid, kLaneThreads, 0, s>>>(a);
   return hipGetLastError();

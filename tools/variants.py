@@ -388,6 +388,17 @@ VARIANTS["lane_sidezero"] = [
     ("crc32c_kernels.hip",
      "      ED[sl] = asm_load_u32(owned && lastk && vtb != 0u && (vqe & 31u) == 0u ? vp + vlen - 4u : zero);\n",
      "      ED[sl] = asm_load_u32(zero);\n")] + MEASURE_ONLY
+# ... or without them at all, with and without the fold of clean lines
+VARIANTS["lane_noside"] = [
+    ("crc32c_kernels.hip", "      HD[sl] = asm_load_u32(owned && t.k == 0 && vq0 == 0u && vh != 0u ? vp & ~3ull : zero);\n",
+     "      HD[sl] = 0u;\n"),
+    ("crc32c_kernels.hip",
+     "      if (kVerify && hdr) SC[sl] = asm_load_u32(owned && t.k == 0 && 4u * vq0 < vh + kLogCrcBack ? vp - kLogCrcBack : zero);\n",
+     "      SC[sl] = 0u;\n"),
+    ("crc32c_kernels.hip",
+     "      ED[sl] = asm_load_u32(owned && lastk && vtb != 0u && (vqe & 31u) == 0u ? vp + vlen - 4u : zero);\n",
+     "      ED[sl] = 0u;\n")] + MEASURE_ONLY
+VARIANTS["lane_bare"] = VARIANTS["lane_noside"] + VARIANTS["lane_nofold"][:1]
 VARIANTS["lane_noout"] =[("crc32c_kernels.hip", "        if (a.out != nullptr) __builtin_nontemporal_store(v, a.out + rec);\n",
                            "")] + MEASURE_ONLY
 # the lane kernel at 12 / 16 waves per CU
@@ -395,6 +406,9 @@ VARIANTS["lane_w12"] = [("crc32c_kernels.hip", "constexpr uint32_t kLaneThreads 
 VARIANTS["lane_w16"] = [("crc32c_kernels.hip", "constexpr uint32_t kLaneThreads = 512;", "constexpr uint32_t kLaneThreads = 1024;")]
 # the lane kernel before the partial-line mask (round 5's committed kernels)
 VARIANTS["lane_r05"] = [("crc32c_kernels.hip", "@git", "7af4fee:prismdb_amd/csrc/crc32c_kernels.hip")]
+# the lane path before the long-span list moved to the side stream (710a890)
+VARIANTS["lane_710a"] = [(f, "@git", "710a890:prismdb_amd/csrc/" + f)
+                         for f in ("crc32c_kernels.hip", "crc32c_capi.hip", "crc32c_device.h")]
 # combinations
 VARIANTS["w111"] = [("crc32c_direct.hip", "constexpr uint32_t kRunWeight[3] = {8u, 7u, 6u};",
                      "constexpr uint32_t kRunWeight[3] = {1u, 1u, 1u};")]
