@@ -409,6 +409,10 @@ VARIANTS["lane_r05"] = [("crc32c_kernels.hip", "@git", "7af4fee:prismdb_amd/csrc
 # the lane path before the long-span list moved to the side stream (710a890)
 VARIANTS["lane_710a"] = [(f, "@git", "710a890:prismdb_amd/csrc/" + f)
                          for f in ("crc32c_kernels.hip", "crc32c_capi.hip", "crc32c_device.h")]
+# the sealing lane kernel issuing its side loads only with a run's first /
+# last task, as the verify kernel does
+VARIANTS["lane_seal_cond"] = [("crc32c_kernels.hip", "    constexpr bool kSideAlways = !kVerify;\n",
+                               "    constexpr bool kSideAlways = false;\n")]
 # combinations
 VARIANTS["w111"] = [("crc32c_direct.hip", "constexpr uint32_t kRunWeight[3] = {8u, 7u, 6u};",
                      "constexpr uint32_t kRunWeight[3] = {1u, 1u, 1u};")]
