@@ -413,6 +413,16 @@ VARIANTS["lane_710a"] = [(f, "@git", "710a890:prismdb_amd/csrc/" + f)
 # last task, as the verify kernel does
 VARIANTS["lane_seal_cond"] = [("crc32c_kernels.hip", "    constexpr bool kSideAlways = !kVerify;\n",
                                "    constexpr bool kSideAlways = false;\n")]
+# the lane kernel with one task in flight per wave (every wait drains: the
+# next task's loads go out only after the fold) at 8 / 12 / 16 waves per CU:
+# do more waves hide the fold better than the two-slot ring?
+LANE_W1 = [("crc32c_kernels.hip", '  asm volatile("s_waitcnt vmcnt(8)"\n               : "+v"(w[0])',
+            '  asm volatile("s_waitcnt vmcnt(0)"\n               : "+v"(w[0])')]
+VARIANTS["lane_w8_1"] = LANE_W1
+VARIANTS["lane_w12_1"] = LANE_W1 + VARIANTS["lane_w12"]
+VARIANTS["lane_w16_1"] = LANE_W1 + VARIANTS["lane_w16"]
+# the lane kernel before zero-region chunks (the committed HEAD's kernels)
+VARIANTS["lane_head"] = [("crc32c_kernels.hip", "@git", "HEAD:prismdb_amd/csrc/crc32c_kernels.hip")]
 # combinations
 VARIANTS["w111"] = [("crc32c_direct.hip", "constexpr uint32_t kRunWeight[3] = {8u, 7u, 6u};",
                      "constexpr uint32_t kRunWeight[3] = {1u, 1u, 1u};")]
