@@ -48,6 +48,7 @@ import ctypes
 import glob
 import json
 import os
+import re
 import socket
 import subprocess
 import sys
@@ -283,10 +284,15 @@ def cpu_baseline_leg(args, gpu_out, dev_buf) -> dict | None:
 def load_pmc_traffic(nblocks: int):
     """HBM bytes per launch of the span kernel from the committed PMC profile
     (profiles/*pmc*.json, written by tools/pmc_summary.py), if it matches."""
-    best = None  # the last match in path order: profiles/r04/... after profiles/r03...
+    best = None  # the newest match: rNN round, then the run tag (r05ab after r05g after r05a)
+
+    def order(p):
+        m = re.match(r"r(\d+)([a-z]*)", os.path.basename(p))
+        return (int(m.group(1)), len(m.group(2)), m.group(2)) if m else (-1, 0, p)
+
     paths = glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")) + \
         glob.glob(os.path.join(ROOT, "profiles", "*", "*pmc*.json"))
-    for p in sorted(paths):
+    for p in sorted(paths, key=order):
         try:
             with open(p) as f:
                 d = json.load(f)
