@@ -1055,7 +1055,47 @@ def test_short_records_far_apart(dev, oracle, short_route):
     torch.cuda.empty_cache()
 
 
-def test_planner_workspace_across_stream_counts(dev, oracle, native):
+@pytest.mark.parametrize("layout", ["runs", "all_long", "one_short_run", "under_a_run"])
+def test_lane_runs_without_owned_records(dev, oracle, native, layout):
+    """Log-record batches on the lane route whose runs of 64 spans hold no
+    record the lane kernel owns (all > 1280 B): the lane kernel visits every
+    run (it no longer skips them by a flag) and reads the zero region there,
+    while the long-span list -- built on the side stream next to it -- sends
+    those records through the generic path.  Whole long runs, whole short
+    runs and mixed ones; a batch of long records only; one short run among
+    long ones; fewer spans than a run.  Bit-exact, verify flags included."""
+    import torch
+    from conftest import set_route
+    from prismdb_amd import crc32c
+
+    rng = np.random.default_rng(0x5EED0060)
+    kinds = {"runs": ["L"] * 64 + ["S"] * 64 + ["L"] * 30 + ["S"] * 34 + ["L"] * 128 + ["S"] * 17,
+             "all_long": ["L"] * 200,
+             "one_short_run": ["L"] * 192 + ["S"] * 64 + ["L"] * 64,
+             "under_a_run": ["L"] * 20 + ["S"] * 9}[layout]
+    lens = np.array([rng.integers(1281, 9000) if k == "L" else rng.integers(8, 1281) for k in kinds], dtype=np.uint64)
+    n = len(lens)
+    gaps = rng.integers(7, 40, size=n).astype(np.uint64)
+    off = np.cumsum(np.concatenate([[13], (lens + gaps)[:-1]])).astype(np.uint64)
+    host = oracle.synth(int(off[-1] + lens[-1]) + 64, 0x5EED0061)
+    raw, _ = oracle.batch(host, off, lens)
+    damaged = rng.random(n) < 0.2
+    for i in range(n):  # stored crc 6 B before each span (log::Writer's header)
+        c = oracle.mask(int(raw[i])) ^ (2 if damaged[i] else 0)
+        host[int(off[i]) - 6:int(off[i]) - 2] = np.frombuffer(np.uint32(c).tobytes(), dtype=np.uint8)
+    want, _ = oracle.batch(host, off, lens, mask=True)
+    buf = torch.from_numpy(host).to(dev)
+    d_off = torch.from_numpy(off.astype(np.int64)).to(dev)
+    d_len = torch.from_numpy(lens.astype(np.uint32).view(np.int32)).to(dev)
+    restore = set_route(native, "lane_log")
+    try:
+        out, mm = crc32c.batch(buf, d_off, d_len, mask=True, verify=True, log_header=True)
+        listed = _last_split(native)[3]
+    finally:
+        restore()
+    np.testing.assert_array_equal(_u32(out), want)
+    np.testing.assert_array_equal(mm.cpu().numpy(), damaged.astype(np.uint8))
+    assert listed == kinds.count("L")
     """One caller stream, three planner-path batches in a row reusing one
     workspace: spans that are not log records, then the same spans as log
     records (the lane kernel and its list in front), then the first batch
