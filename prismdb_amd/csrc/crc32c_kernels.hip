@@ -1280,12 +1280,11 @@ __global__ __launch_bounds__(kLaneThreads) void crc32c_lane_kernel(SpanBatch a) 
   const StrideLanes tab = stride_lanes(lane);
   const uint32_t wave = rfl(blockIdx.x * (kLaneThreads / 64u) + (tid >> 6));
   const uint32_t nwaves = gridDim.x * (kLaneThreads / 64u);
-  // Every run of the batch: one whose spans the kernel owns none of costs
-  // one task of loads from the zero region.  (Runs used to be skipped by a
-  // flag from crc32c_long_list_kernel, which then had to finish first; it
-  // now runs next to this kernel.)
-  auto next_run = [&](uint32_t rb) -> uint32_t { return rb; };
-  const uint32_t first = next_run(wave * 64u);
+  // Every run of the batch, in turn: one whose spans the kernel owns none of
+  // costs one task of loads from the zero region.  (Runs used to be skipped
+  // by a flag from crc32c_long_list_kernel, which then had to finish first;
+  // it now runs next to this kernel.)
+  const uint32_t first = wave * 64u;
   if (first >= n) return;
   // Priority rotation by SIMD age rank (two waves per SIMD here), as in
   // crc32c_pair_kernel: one step per run (WAL verify +1.1-1.3 %, seal
@@ -1343,7 +1342,7 @@ __global__ __launch_bounds__(kLaneThreads) void crc32c_lane_kernel(SpanBatch a) 
       // the lines holding a record's last body word short of the line's end
       // (a record ending exactly at a line's end has no such line)
       t.pm = wave_reduce<2>(owned && (qe & 31u) != 0u ? 1u << (qe >> 5) : 0u);
-      t.nrb = next_run(t.rb + 64u * nwaves);
+      t.nrb = t.rb + 64u * nwaves;
       prio ^= 1u;
       if (prio == 0u) __builtin_amdgcn_s_setprio(0);
       else __builtin_amdgcn_s_setprio(1);
@@ -1353,7 +1352,8 @@ __global__ __launch_bounds__(kLaneThreads) void crc32c_lane_kernel(SpanBatch a) 
     // The verify kernel issues them only there (WAL verify +6.8 % against
     // issuing them with every task, from a zero region when unused:
     // profiles/r02s3w_*); the sealing kernel issues them with every task
-    // (2.5 % faster that way in the same A/B).  Loads written under branches:
+    // (2.5 % faster that way in the same A/B; neutral in round 5,
+    // profiles/r05/r05w_variants_lane_merged_side_load.json).  Loads written under branches:
     // at 16 waves hipcc, short of VGPRs, copied such registers at the merge
     // before their wait; the CFG audit run by build() fails on any such touch,
     // and this build has none.
@@ -1362,9 +1362,8 @@ __global__ __launch_bounds__(kLaneThreads) void crc32c_lane_kernel(SpanBatch a) 
     // not the one the task loads (see fold: the head dword precedes a body
     // that starts a line, a log header's crc lies in the line before, the
     // tail bytes follow a body that ends a line); every other lane's address
-    // is the wave's zero region -- one line for the whole instruction instead
-    // of 64 (WAL verify +2.1 %, profiles/r05/r05s_variants_lane_side_dwords.json;
-    // without the side loads at all it would gain 6.6 %: r05r_variants_lane_diagnosis.json).
+    // is the wave's zero region (WAL verify +2.1 %,
+    // profiles/r05/r05s_variants_lane_side_dwords.json).
     constexpr bool kSideAlways = !kVerify;
     const bool live = t.rb < n;
     const bool owned = live && ((vmeta >> 25) & 1u);
