@@ -94,3 +94,28 @@ def test_multi_leg_child_reports_instead_of_raising(monkeypatch):
     args.multi_timeout = 0.01
     res = bench.run_multi_child(args, 2)
     assert res == {"devices": 2, "error": "batch_multi leg stopped after 0 s"}
+
+
+def test_pmc_summary_picked_is_the_newest():
+    """The line's `traffic` comes from the newest committed PMC summary of
+    the headline workload: by round, then run tag (r05ab after r05g after
+    r05a), not by plain path order (where r05ab sorts before r05g)."""
+    import glob
+    import re
+
+    bench = _bench_module()
+    got = bench.load_pmc_traffic(1 << 24)
+    assert got is not None
+
+    def key(p):
+        m = re.match(r"r(\d+)([a-z]*)", os.path.basename(p))
+        return (int(m.group(1)), len(m.group(2)), m.group(2))
+
+    cands = []
+    for p in glob.glob(os.path.join(ROOT, "profiles", "*", "r*_pmc.json")):
+        with open(p) as f:
+            d = json.load(f)
+        if d.get("nblocks") == 1 << 24 and d.get("hbm_bytes_per_launch"):
+            cands.append(p)
+    assert key("r05ab_pmc.json") > key("r05g_pmc.json") > key("r05a_pmc.json")
+    assert os.path.basename(got["_path"]) == os.path.basename(max(cands, key=key))
