@@ -423,6 +423,40 @@ VARIANTS["lane_w12_1"] = LANE_W1 + VARIANTS["lane_w12"]
 VARIANTS["lane_w16_1"] = LANE_W1 + VARIANTS["lane_w16"]
 # the lane kernel before zero-region chunks (the committed HEAD's kernels)
 VARIANTS["lane_head"] = [("crc32c_kernels.hip", "@git", "HEAD:prismdb_amd/csrc/crc32c_kernels.hip")]
+# the trailer pass (planner-path sealing): measurement-only (neighbouring
+# bytes rewritten unguarded: wrong for spans < 32 B apart) -- each trailer
+# written as the whole aligned 32-B sector(s) around it, read first, instead
+# of one 4-B partial write: do full-sector writes beat the partial ones?
+TRAIL_STORE = "    store_le32(t, res[i]);\n  }\n}\n"
+VARIANTS["trail_sector"] = [("crc32c_kernels.hip", TRAIL_STORE,
+    "    {\n"
+    "      const uint64_t ta = reinterpret_cast<uint64_t>(t), s0 = ta & ~31ull, s1 = (ta + 3u) & ~31ull;\n"
+    "      const uint32_t v = res[i];\n"
+    "      for (uint64_t sa = s0; sa <= s1; sa += 32u) {\n"
+    "        uint32_t w[8];\n"
+    "        for (int k = 0; k < 8; ++k) w[k] = reinterpret_cast<const uint32_t*>(sa)[k];\n"
+    "        for (int k = 0; k < 8; ++k) {\n"
+    "          const int64_t d = (int64_t)(sa + 4u * k) - (int64_t)ta;  // word k's offset from the trailer\n"
+    "          uint64_t x = (uint64_t)w[k];\n"
+    "          for (int b = 0; b < 4; ++b) {\n"
+    "            const int64_t j = d + b;\n"
+    "            if (j >= 0 && j < 4) x = (x & ~(0xFFull << (8 * b))) | ((uint64_t)((v >> (8 * j)) & 0xFFu) << (8 * b));\n"
+    "          }\n"
+    "          w[k] = (uint32_t)x;\n"
+    "        }\n"
+    "        typedef uint32_t v4t __attribute__((ext_vector_type(4)));\n"
+    "        reinterpret_cast<v4t*>(sa)[0] = v4t{w[0], w[1], w[2], w[3]};\n"
+    "        reinterpret_cast<v4t*>(sa)[1] = v4t{w[4], w[5], w[6], w[7]};\n"
+    "      }\n"
+    "    }\n  }\n}\n")] + MEASURE_ONLY
+# the trailer pass in 128-thread blocks (twice the blocks)
+VARIANTS["trail_b128"] = [("crc32c_kernels.hip",
+    "  const uint64_t blocks = (a.n + 255u) / 256u;\n  const int grid = (int)(blocks < 16384u ? blocks : 16384u);\n"
+    "  if (desc) crc32c_trailer_kernel<true><<<grid, 256, 0, s>>>(a, res);\n"
+    "  else crc32c_trailer_kernel<false><<<grid, 256, 0, s>>>(a, res);\n",
+    "  const uint64_t blocks = (a.n + 127u) / 128u;\n  const int grid = (int)(blocks < 32768u ? blocks : 32768u);\n"
+    "  if (desc) crc32c_trailer_kernel<true><<<grid, 128, 0, s>>>(a, res);\n"
+    "  else crc32c_trailer_kernel<false><<<grid, 128, 0, s>>>(a, res);\n")]
 # combinations
 VARIANTS["w111"] = [("crc32c_direct.hip", "constexpr uint32_t kRunWeight[3] = {8u, 7u, 6u};",
                      "constexpr uint32_t kRunWeight[3] = {1u, 1u, 1u};")]
