@@ -7,6 +7,8 @@
 // task's loads issued before the current task is folded):
 //   lane   one record per lane; a task is one line of each of the wave's 64
 //          records (eight 16-B loads per lane), folded as one 32-step chain
+//          (modes 2 / 3: as two / four independent chains, joined by one
+//          more step each)
 //   octet  8 lanes per record; a task is every line of each of the wave's 8
 //          records (one 16-B load per lane and line: each instruction reads 8
 //          whole lines), folded as four column chains per lane, then joined
@@ -32,6 +34,7 @@ __device__ __forceinline__ void fill(uint32_t* lds) {
   __syncthreads();
 }
 
+template <int kChains>  // independent chains per line (joined by one more step each)
 __global__ __launch_bounds__(512) void lane_fold(const uint8_t* __restrict__ p, uint64_t nrec, uint32_t stride,
                                                  uint32_t len, uint32_t* __restrict__ out) {
   __shared__ uint32_t lds[kTabWords];
@@ -57,8 +60,18 @@ __global__ __launch_bounds__(512) void lane_fold(const uint8_t* __restrict__ p, 
 #pragma unroll
         for (int j = 0; j < 8; ++j) b[j] = *reinterpret_cast<const v4*>(p + line(t + 1) + 16 * j);
       }
+      constexpr int q = 32 / kChains;
+      uint32_t ch[kChains];
+      ch[0] = x;
 #pragma unroll
-      for (int i = 0; i < 32; ++i) x = stp(lds, c, x, a[i >> 2][i & 3]);
+      for (int k = 1; k < kChains; ++k) ch[k] = 0u;
+#pragma unroll
+      for (int i = 0; i < q; ++i)
+#pragma unroll
+        for (int k = 0; k < kChains; ++k) ch[k] = stp(lds, c, ch[k], a[(k * q + i) >> 2][(k * q + i) & 3]);
+      x = ch[0];
+#pragma unroll
+      for (int k = 1; k < kChains; ++k) x = stp(lds, c, x, ch[k]);
 #pragma unroll
       for (int j = 0; j < 8; ++j) a[j] = b[j];
     }
@@ -145,7 +158,9 @@ extern "C" int recfold(const void* p, uint64_t nrec, uint32_t stride, uint32_t l
   hipStream_t s = (hipStream_t)stream;
   const uint8_t* b = (const uint8_t*)p;
   if (len == 0 || len > 1280u) return -2;
-  if (mode == 0) lane_fold<<<grid, 512, 0, s>>>(b, nrec, stride, len, out);
+  if (mode == 0) lane_fold<1><<<grid, 512, 0, s>>>(b, nrec, stride, len, out);
+  else if (mode == 2) lane_fold<2><<<grid, 512, 0, s>>>(b, nrec, stride, len, out);
+  else if (mode == 3) lane_fold<4><<<grid, 512, 0, s>>>(b, nrec, stride, len, out);
   else {
     const uint32_t lines = (127u + len + 127u) / 128u;  // the most lines a record of len bytes spans
     if (lines <= 3) octet_fold<3><<<grid, 512, 0, s>>>(b, nrec, stride, len, out);

@@ -62,7 +62,7 @@ def main():
         assert rc == 0
         return e0.elapsed_time(e1) / 1e3
 
-    names = {0: "lane_fold", 1: "octet_fold"}
+    names = {0: "lane_fold", 2: "lane_fold_2ch", 3: "lane_fold_4ch", 1: "octet_fold"}
     for m in names:
         timed(m)
     res = {v: [] for v in names.values()}
