@@ -607,17 +607,29 @@ def multi_leg(args, torch, crc32c, ndev: int) -> dict:
     res = {"devices": ndev, "clique": ndev, "files_per_device": nfiles, "spans_per_device": n,
            "steps": args.c5_steps, "call": "one leveldb_crc32c_batch_multi per step: every partition sealed "
            "(MASK | WRITE_TRAILER) on its device, results gathered to device 0"}
-    for name, fn in (("with_gather", gathered), ("without_gather", separate)):
+    # Three rounds of c5_steps steps per leg, the legs alternating (a leg
+    # timed right after the other ran up to 10 % apart from run to run; the
+    # per-call hand-offs cost ~2 %: tools/multi_ab.py, profiles/r05/r05an_multi_ab.json);
+    # each leg's median round.
+    legs = (("with_gather", gathered), ("without_gather", separate))
+    for _, fn in legs:
         fn()
-        sync_all()
-        t0 = time.perf_counter()
-        for _ in range(args.c5_steps):
-            fn()
-        sync_all()
-        el = time.perf_counter() - t0
+    sync_all()
+    rounds = {name: [] for name, _ in legs}
+    for r in range(3):
+        for name, fn in (legs if r % 2 == 0 else legs[::-1]):
+            t0 = time.perf_counter()
+            for _ in range(args.c5_steps):
+                fn()
+            sync_all()
+            rounds[name].append(time.perf_counter() - t0)
+    for name, fn in legs:
+        el = sorted(rounds[name])[1]
         res[name] = {"value": round(ndev * nfiles * span_bytes * args.c5_steps / el / GIB, 2), "unit": "GiB/s",
-                     "ms_per_step": round(el * 1e3 / args.c5_steps, 3)}
+                     "ms_per_step": round(el * 1e3 / args.c5_steps, 3), "rounds": 3, "stat": "median round"}
         if name == "with_gather":
+            fn()  # the timing diagnostics below read this call's phases
+            sync_all()
             # the last step's phases on each device (HIP events on the clique
             # streams) and the clique's one-time ncclCommInitAll
             tm = crc32c.multi_timing(list(range(ndev)))

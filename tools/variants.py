@@ -457,6 +457,23 @@ VARIANTS["trail_b128"] = [("crc32c_kernels.hip",
     "  const uint64_t blocks = (a.n + 127u) / 128u;\n  const int grid = (int)(blocks < 32768u ? blocks : 32768u);\n"
     "  if (desc) crc32c_trailer_kernel<true><<<grid, 128, 0, s>>>(a, res);\n"
     "  else crc32c_trailer_kernel<false><<<grid, 128, 0, s>>>(a, res);\n")]
+# batch_multi without its per-call timing events (t0 / t1 / t2 on the clique
+# streams; prismdb_crc32c_multi_timing then reports nothing) -- what they cost
+VARIANTS["multi_notime"] = [
+    ("crc32c_multi.hip", "    if ((e = hipEventRecord(c->t0[p], c->streams[p])) != hipSuccess) return finish(HipFail(e, \"hipEventRecord\"));\n", ""),
+    ("crc32c_multi.hip", "    if ((e = hipEventRecord(c->t1[p], c->streams[p])) != hipSuccess) return finish(HipFail(e, \"hipEventRecord\"));\n", ""),
+    ("crc32c_multi.hip", "    if ((e = hipEventRecord(c->t2[p], c->streams[p])) != hipSuccess) return finish(HipFail(e, \"hipEventRecord\"));\n", ""),
+    ("crc32c_multi.hip", "  c->timed = true;\n", "")]
+# batch_multi with one device run straight on the caller's stream (no clique
+# stream hand-offs) -- what the hand-offs cost
+VARIANTS["multi_direct1"] = [
+    ("crc32c_multi.hip", "  Clique* c = nullptr;\n  int rc = GetClique(ndev, devices, &c);\n",
+     "  if (ndev == 1) {\n"
+     "    if ((e = hipSetDevice(devices[0])) != hipSuccess) return HipFail(e, \"hipSetDevice\");\n"
+     "    const int r1 = n[0] == 0 ? 0 : leveldb_crc32c_batch(dev_base[0], dev_off[0], dev_len[0], dev_init != nullptr ? dev_init[0] : nullptr,\n"
+     "                                      n[0], out0, mismatch0, flags, streams != nullptr ? streams[0] : nullptr);\n"
+     "    (void)hipSetDevice(cur);\n    return r1;\n  }\n"
+     "  Clique* c = nullptr;\n  int rc = GetClique(ndev, devices, &c);\n")]
 # combinations
 VARIANTS["w111"] = [("crc32c_direct.hip", "constexpr uint32_t kRunWeight[3] = {8u, 7u, 6u};",
                      "constexpr uint32_t kRunWeight[3] = {1u, 1u, 1u};")]
