@@ -709,6 +709,7 @@ int RunBatch(DeviceCtx& ctx, const SpanBatch& base_args, bool desc, bool verify,
     if (e == hipSuccess) e = prismdb::dev::launch_long_list(a, ws, w->side);
     if (e == hipSuccess) e = hipEventRecord(w->join, w->side);
     if (e != hipSuccess) return FailHip(e, "long-span list launch");
+    a.claim = &ws.counters->lane_claim;  // (zeroed with the counters above)
     e = prismdb::dev::launch_lane(a, verify, ctx.cus, s);
     if (e == hipSuccess) e = hipStreamWaitEvent(s, w->join, 0);
     if (e != hipSuccess) return FailHip(e, "lane kernel launch");

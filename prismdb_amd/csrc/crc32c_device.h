@@ -100,7 +100,8 @@ struct SpanBatch {
   // when the scan finds every record one task; the general kernel then leaves).
   uint32_t pair_kernel;
   // nullable, zero at launch: the span kernel's claim counter for its last
-  // kTailRounds rounds of slices or runs (dealt on demand, not statically)
+  // kTailRounds rounds of slices or runs (dealt on demand, not statically);
+  // the lane kernel's for its last rounds of runs
   uint32_t* claim;
   const unsigned long long* tasks_dev;  // nullable: the span pass's chunk tasks (slice scan)
 };
@@ -118,6 +119,7 @@ struct SplitCounters {
   unsigned long long nlist;             // spans the lane kernel leaves to the generic path
   unsigned long long slice_q, slice_r;  // exact slices: q = T / K, r = T % K
   uint32_t claim;                       // span kernel: tail slices claimed (SpanBatch::claim)
+  uint32_t lane_claim;                  // lane kernel: tail runs claimed (its SpanBatch::claim)
 };
 
 struct SplitWs {

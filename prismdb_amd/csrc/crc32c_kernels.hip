@@ -59,6 +59,13 @@ constexpr uint32_t kRunsPerStream = 64;  // span kernel: one-task runs shrink un
 // sat between (and cost 4 KiB descriptors 2 %), 2 and 4 ran no faster.
 constexpr uint32_t kTailRounds = 12;
 constexpr uint32_t kPairTailRounds = 16;
+// The lane kernel's last rounds of runs of 64 records, claimed on demand:
+// on ~1 KB WAL records its waves left 3542-3890 us into a 3.9 ms kernel,
+// rank-1 waves 1.7 % and some XCDs 4.5 % behind the others
+// (profiles/r05/r05aq_lane_timeline.json).  8 rounds against none: WAL
+// verify +2.9 %, seal +1.6 % (4: +1.8 %, 12: +2.6 %;
+// profiles/r05/r05ar_variants_lane_tail.json).
+constexpr uint32_t kLaneTailRounds = 8;
 }  // namespace
 }  // namespace dev
 }  // namespace prismdb
@@ -1283,7 +1290,22 @@ __global__ __launch_bounds__(kLaneThreads) void crc32c_lane_kernel(SpanBatch a) 
   // Every run of the batch, in turn: one whose spans the kernel owns none of
   // costs one task of loads from the zero region.  (Runs used to be skipped
   // by a flag from crc32c_long_list_kernel, which then had to finish first;
-  // it now runs next to this kernel.)
+  // it now runs next to this kernel.)  Runs [0, Rs) are dealt round-robin;
+  // the last kLaneTailRounds rounds are claimed from a per-call counter as
+  // waves run out (the atomic's return drains the wave's ring once per
+  // claimed run: the compiler waits for it with vmcnt(0)).
+  const uint32_t R = (n + 63u) >> 6;
+  const uint32_t tailr = a.claim != nullptr && R > (kLaneTailRounds + 2u) * nwaves ? kLaneTailRounds * nwaves : 0u;
+  const uint32_t Rs = R - tailr;
+  auto run_after = [&](uint32_t rb) -> uint32_t {  // the wave's next run after run rb (n: none)
+    uint32_t nx = (rb >> 6) + nwaves;
+    if (tailr != 0u && nx >= Rs) {
+      uint32_t got = 0;
+      if (lane == 0u) got = __hip_atomic_fetch_add(a.claim, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      nx = Rs + rfl(got);
+    }
+    return nx < R ? nx << 6 : n;
+  };
   const uint32_t first = wave * 64u;
   if (first >= n) return;
   // Priority rotation by SIMD age rank (two waves per SIMD here), as in
@@ -1342,7 +1364,7 @@ __global__ __launch_bounds__(kLaneThreads) void crc32c_lane_kernel(SpanBatch a) 
       // the lines holding a record's last body word short of the line's end
       // (a record ending exactly at a line's end has no such line)
       t.pm = wave_reduce<2>(owned && (qe & 31u) != 0u ? 1u << (qe >> 5) : 0u);
-      t.nrb = t.rb + 64u * nwaves;
+      t.nrb = run_after(t.rb);
       prio ^= 1u;
       if (prio == 0u) __builtin_amdgcn_s_setprio(0);
       else __builtin_amdgcn_s_setprio(1);

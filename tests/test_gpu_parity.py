@@ -1055,6 +1055,45 @@ def test_short_records_far_apart(dev, oracle, short_route):
     torch.cuda.empty_cache()
 
 
+def test_lane_claimed_tail_runs(dev, oracle, native):
+    """A log-record batch large enough for the lane kernel's claimed tail
+    (more than (kLaneTailRounds + 2) runs of 64 records per wave: its last
+    rounds of runs are claimed from a per-call counter): 1.6 M short records
+    with a few long ones among them (the generic path), every record's
+    result bit-exact and every damaged one flagged."""
+    import torch
+    from conftest import set_route
+    from prismdb_amd import crc32c
+
+    rng = np.random.default_rng(0x5EED0070)
+    n = 1_600_000
+    lens = rng.integers(8, 200, size=n).astype(np.uint64)
+    lens[rng.integers(0, n, size=300)] = rng.integers(1281, 4000, size=300).astype(np.uint64)
+    gaps = rng.integers(7, 20, size=n).astype(np.uint64)
+    off = np.cumsum(np.concatenate([[11], (lens + gaps)[:-1]])).astype(np.uint64)
+    host = oracle.synth(int(off[-1] + lens[-1]) + 64, 0x5EED0071)
+    raw, _ = oracle.batch(host, off, lens)
+    damaged = rng.random(n) < 0.01
+    masked = ((raw.astype(np.uint64) << np.uint64(17) | raw.astype(np.uint64) >> np.uint64(15)) & np.uint64(0xFFFFFFFF))
+    masked = ((masked + np.uint64(0xa282ead8)) & np.uint64(0xFFFFFFFF)).astype(np.uint32) ^ damaged.astype(np.uint32)
+    pos = off.astype(np.int64) - 6
+    view = host[:int(pos[-1]) + 4 + 64]
+    idx = pos[:, None] + np.arange(4)[None, :]
+    view[idx] = masked.view(np.uint8).reshape(-1, 4)
+    want, _ = oracle.batch(host, off, lens, mask=True)
+    buf = torch.from_numpy(host).to(dev)
+    d_off = torch.from_numpy(off.astype(np.int64)).to(dev)
+    d_len = torch.from_numpy(lens.astype(np.uint32).view(np.int32)).to(dev)
+    restore = set_route(native, "lane_log")
+    try:
+        out, mm = crc32c.batch(buf, d_off, d_len, mask=True, verify=True, log_header=True)
+    finally:
+        restore()
+    np.testing.assert_array_equal(_u32(out), want)
+    np.testing.assert_array_equal(mm.cpu().numpy(), damaged.astype(np.uint8))
+    assert oracle.mask(int(raw[0])) == int(masked[0] ^ damaged[0])
+
+
 @pytest.mark.parametrize("layout", ["runs", "all_long", "one_short_run", "under_a_run"])
 def test_lane_runs_without_owned_records(dev, oracle, native, layout):
     """Log-record batches on the lane route whose runs of 64 spans hold no

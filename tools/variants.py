@@ -474,6 +474,22 @@ VARIANTS["multi_direct1"] = [
      "                                      n[0], out0, mismatch0, flags, streams != nullptr ? streams[0] : nullptr);\n"
      "    (void)hipSetDevice(cur);\n    return r1;\n  }\n"
      "  Clique* c = nullptr;\n  int rc = GetClique(ndev, devices, &c);\n")]
+# measurement: the lane kernel's per-wave entry and exit (tools/wave_timeline.py --work wal)
+VARIANTS["lane_ts"] = [
+    ("crc32c_kernels.hip", "  const uint32_t first = wave * 64u;\n  if (first >= n) return;\n",
+     "  const uint32_t first = wave * 64u;\n  if (first >= n) return;\n  const uint64_t ts0 = __builtin_amdgcn_s_memrealtime();\n"),
+    ("crc32c_kernels.hip",
+     "    asm volatile(\"\" : \"+v\"(HD[sl]), \"+v\"(ED[sl]), \"+v\"(SC[sl]));\n  }\n  asm volatile(\"\" : \"+v\"(noff), \"+v\"(nlen), \"+v\"(ninit));\n}\n",
+     "    asm volatile(\"\" : \"+v\"(HD[sl]), \"+v\"(ED[sl]), \"+v\"(SC[sl]));\n  }\n  asm volatile(\"\" : \"+v\"(noff), \"+v\"(nlen), \"+v\"(ninit));\n"
+     "  if (a.out != nullptr && lane < 2u) {\n"
+     "    const uint64_t ts1 = __builtin_amdgcn_s_memrealtime();\n"
+     "    reinterpret_cast<uint64_t*>(a.out + ((n + 3u) & ~3u))[2u * wave + lane] = lane == 0u ? ts0 : ts1;\n"
+     "  }\n}\n"),
+] + MEASURE_ONLY
+# the lane kernel's claimed tail of runs: none / 4 / 12 rounds (product: 8)
+for _r in (0, 4, 12):
+    VARIANTS[f"lane_tail{_r}"] = [("crc32c_kernels.hip", "constexpr uint32_t kLaneTailRounds = 8;",
+                                   f"constexpr uint32_t kLaneTailRounds = {_r};")]
 # combinations
 VARIANTS["w111"] = [("crc32c_direct.hip", "constexpr uint32_t kRunWeight[3] = {8u, 7u, 6u};",
                      "constexpr uint32_t kRunWeight[3] = {1u, 1u, 1u};")]

@@ -26,9 +26,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--lib", default=os.path.join(ROOT, "tools", "vlib", "lib_pair_ts.so"))
     ap.add_argument("--spans", type=int, default=1 << 24)
-    ap.add_argument("--work", choices=["sst", "fixed", "mixed"], default="sst",
+    ap.add_argument("--work", choices=["sst", "fixed", "mixed", "wal"], default="sst",
                     help="sst: SST descriptors (pair-run kernel); fixed: 16 Mi x 4 KiB fixed blocks (fixed kernel); "
-                         "mixed: config 3's 1/4/16/64 KiB spans, 32 GiB (span kernel)")
+                         "mixed: config 3's 1/4/16/64 KiB spans, 32 GiB (span kernel); "
+                         "wal: ~1 KB log records, 16 GiB, LOG_HEADER verify (lane kernel, 8 waves per CU)")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -62,12 +63,28 @@ def main():
         lens = rng.choice([1024, 4096, 16384, 65536], size=(32 << 30) // 21760).astype(np.int64)
         off = np.concatenate([[0], np.cumsum(lens)[:-1]])
         n = len(off)
-    buf = torch.empty(max(files * fb, n * 4096) + 64, dtype=torch.uint8, device=dev)
+    flags, wpc = 0, 16
+    if args.work == "wal":
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        from bench_configs import build_log
+        from prismdb_amd import log
+
+        fbl = 4 << 20
+        img = build_log(np.random.default_rng(0x5EED0003), fbl)
+        hoff, hlen = log.scan(img)
+        nf = (16 << 30) // fbl
+        off = ((np.arange(nf, dtype=np.int64)[:, None] * fbl + hoff.astype(np.int64)[None, :]) + 6).reshape(-1)
+        lens = np.tile(hlen.astype(np.int64) + 1, nf)
+        n = len(off)
+        flags, wpc = 0x4, 8
+    buf = torch.empty(max(files * fb, n * 4096 if args.work != "wal" else 16 << 30) + 64, dtype=torch.uint8, device=dev)
     crc32c.fill_synthetic(buf, 0x5EED0001)
+    if args.work == "wal":
+        buf[:nf * fbl].view(nf, fbl).copy_(torch.from_numpy(img).to(dev))
     d_off = torch.from_numpy(off).to(dev)
     d_len = torch.from_numpy(lens.astype(np.int32)).to(dev)
     cus = torch.cuda.get_device_properties(0).multi_processor_count
-    nwaves = cus * 16
+    nwaves = cus * wpc
     base = (n + 3) & ~3
     out = torch.zeros(base + 4 * nwaves, dtype=torch.int32, device=dev)
     s = torch.cuda.current_stream()
@@ -75,7 +92,7 @@ def main():
         if args.work == "fixed":
             rc = f(buf.data_ptr(), 4096, 4096, n, 0, out.data_ptr(), None, 0, ctypes.c_void_p(s.cuda_stream))
         else:
-            rc = g(buf.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), None, n, out.data_ptr(), None, 0,
+            rc = g(buf.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), None, n, out.data_ptr(), None, flags,
                    ctypes.c_void_p(s.cuda_stream))
         assert rc == 0
     torch.cuda.synchronize()
@@ -84,12 +101,12 @@ def main():
     t0 = ts[live, 0].min()
     rel = (ts - t0) / 100.0
     ex = rel[live, 1]
-    slot = (np.arange(nwaves) % 16)[live]
+    slot = (np.arange(nwaves) % wpc)[live]
     res = {"work": args.work, "spans": n, "waves": int(live.sum()),
            "entry": {p: round(float(np.percentile(rel[live, 0], p)), 1) for p in (0, 50, 100)},
            "exit": {p: round(float(np.percentile(ex, p)), 1) for p in (0, 10, 50, 90, 100)},
-           "exit_by_slot": [round(float(ex[slot == k].mean()), 1) for k in range(16)],
-           "exit_by_xcd": [round(float(ex[((np.arange(nwaves) // 16)[live] % 8) == x].mean()), 1) for x in range(8)]}
+           "exit_by_slot": [round(float(ex[slot == k].mean()), 1) for k in range(wpc)],
+           "exit_by_xcd": [round(float(ex[((np.arange(nwaves) // wpc)[live] % 8) == x].mean()), 1) for x in range(8)]}
     print(json.dumps(res))
 
 
