@@ -45,16 +45,21 @@ def main():
     dev = torch.device("cuda", 0)
     stream = torch.cuda.current_stream()
 
-    def timed(fn, reps):
+    def timed(fn, reps, k=3):
+        # k calls back to back per timing, as a caller streams them: the
+        # Python wrapper's work for call i+1 overlaps call i on the device
+        # (timed one at a time, the first call's host work sat inside the
+        # events: ~0.1 ms, 3-4 % of a WAL or config-3 call)
         ts = []
         fn()
         for _ in range(reps):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
-            fn()
+            for _ in range(k):
+                fn()
             e1.record(stream)
             e1.synchronize()
-            ts.append(e0.elapsed_time(e1) / 1e3)
+            ts.append(e0.elapsed_time(e1) / 1e3 / k)
         return statistics.median(ts)
 
     res = {}
