@@ -490,6 +490,12 @@ VARIANTS["lane_ts"] = [
 for _r in (0, 4, 12):
     VARIANTS[f"lane_tail{_r}"] = [("crc32c_kernels.hip", "constexpr uint32_t kLaneTailRounds = 8;",
                                    f"constexpr uint32_t kLaneTailRounds = {_r};")]
+# the lane kernel without its priority rotation (now that its tail is claimed)
+VARIANTS["lane_noprio"] = [
+    ("crc32c_kernels.hip", "  uint32_t prio = rfl(tid >> 6) >> 2;\n  if (prio == 0u) __builtin_amdgcn_s_setprio(0);\n  else __builtin_amdgcn_s_setprio(1);\n",
+     "  uint32_t prio = 0u;\n"),
+    ("crc32c_kernels.hip", "      prio ^= 1u;\n      if (prio == 0u) __builtin_amdgcn_s_setprio(0);\n      else __builtin_amdgcn_s_setprio(1);\n",
+     "      (void)prio;\n")]
 # combinations
 VARIANTS["w111"] = [("crc32c_direct.hip", "constexpr uint32_t kRunWeight[3] = {8u, 7u, 6u};",
                      "constexpr uint32_t kRunWeight[3] = {1u, 1u, 1u};")]
