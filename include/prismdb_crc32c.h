@@ -125,6 +125,10 @@ int leveldb_crc32c_batch(const void* dev_base, const uint64_t* dev_off, const ui
  * the span, or with LOG_HEADER the header crc 6 bytes before it -- as
  * TableBuilder::WriteRawBlock appends it (table/table_builder.cc:192-197); the
  * buffer must then be writable and no trailer may overlap a span of the batch.
+ * The `const` of host_base does not hold under WRITE_TRAILER (nor does that of
+ * dev_base in the device calls): the first and last trailer slots are probed
+ * first, and a buffer not writable there (a PROT_READ mapping) is refused with
+ * PRISMDB_CRC32C_EINVAL before anything is stored.
  * On an error return, the trailers of chunks already finished may be written.
  * Uses the current HIP device.
  */

@@ -80,6 +80,9 @@ def _declare(lib: ctypes.CDLL) -> None:
         "prismdb_crc32c_multi_fail_after": (ctypes.c_int, [ctypes.c_int]),
         "prismdb_crc32c_windows": (ctypes.c_int, [ctypes.c_int]),
         "prismdb_crc32c_multi_timing": (ctypes.c_int, [ctypes.c_int, vp, vp, vp, vp]),
+        "prismdb_crc32c_multi_host_timing": (ctypes.c_int, [ctypes.c_int, vp, vp, vp, vp]),
+        "prismdb_crc32c_multi_self_gather": (ctypes.c_int, [ctypes.c_int]),
+        "prismdb_crc32c_last_claims": (ctypes.c_int, [vp]),
         "prismdb_test_hooks_enabled": (ctypes.c_int, []),
     }
     for name, (res, args) in sig.items():

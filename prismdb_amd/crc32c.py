@@ -272,6 +272,21 @@ def multi_timing(devices):
             "init_ms": round(init.value, 1)}
 
 
+def multi_host_timing(devices):
+    """Host wall times of the last batch_multi call on this device list
+    (diagnostics): {"start_us": [per device: call entry to the start of that
+    partition's enqueue], "enqueue_us": [per device: the enqueue itself --
+    hand-off, scratch, batch launches], "call_us": the whole call}, or None."""
+    ndev = len(devices)
+    c_dev = (ctypes.c_int * ndev)(*devices)
+    st, en = (ctypes.c_double * ndev)(), (ctypes.c_double * ndev)()
+    call = ctypes.c_double(0)
+    if lib().prismdb_crc32c_multi_host_timing(ndev, c_dev, st, en, ctypes.byref(call)) != 0:
+        return None
+    return {"start_us": [round(x, 1) for x in st], "enqueue_us": [round(x, 1) for x in en],
+            "call_us": round(call.value, 1)}
+
+
 def batch_host(base, off, lens, init=None, *, mask: bool = False, verify: bool = False, log_header: bool = False,
                trailer: bool = False):
     """Host-resident batch: numpy (or pinned torch CPU tensor) buffer and
@@ -294,6 +309,17 @@ def batch_host(base, off, lens, init=None, *, mask: bool = False, verify: bool =
     ini = np.ascontiguousarray(init, dtype=np.uint32) if init is not None else None
     if len(lens) != n or (ini is not None and len(ini) != n):
         raise ValueError("off, lens and init must have the same length")
+    # nbytes and the base pointer below assume one contiguous buffer; sealing
+    # also writes into it (the C side refuses a read-only mapping, but a
+    # read-only numpy view of a bytes object is writable memory it must not touch)
+    if hasattr(base, "data_ptr"):
+        if base.is_cuda or not base.is_contiguous():
+            raise ValueError("batch_host: base must be a contiguous host tensor")
+    else:
+        if not base.flags.c_contiguous:
+            raise ValueError("batch_host: base must be a C-contiguous array")
+        if trailer and not base.flags.writeable:
+            raise ValueError("batch_host: trailer=True writes into base, which is read-only")
     nbytes = base.numel() * base.element_size() if hasattr(base, "data_ptr") else base.nbytes
     if n:
         lead, tail = _span_reach(log_header, verify, trailer)

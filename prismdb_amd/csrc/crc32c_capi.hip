@@ -618,6 +618,19 @@ int RunBatch(DeviceCtx& ctx, const SpanBatch& base_args, bool desc, bool verify,
       if (!by_launch) (void)hipEventRecord(w->done[w->gen & 1u], s);
     }
   } mark{w, s};
+  // Between a fork onto the workspace's side stream and its join, an error
+  // return still joins the side stream back into s (before `mark` records
+  // the done event, which must cover the side stream's kernels: the next
+  // call's growth or reuse of the lists and segment records waits on it).
+  struct SideJoin {
+    Workspace* w;
+    hipStream_t s;
+    bool armed = false;
+    ~SideJoin() {
+      if (armed && (hipEventRecord(w->join, w->side) != hipSuccess || hipStreamWaitEvent(s, w->join, 0) != hipSuccess))
+        (void)hipStreamSynchronize(w->side);
+    }
+  } side_join{w, s};
   const bool direct = desc && (route == kRouteDirect ||
                                (route == kRouteAuto && a.n <= g_direct_max.load(std::memory_order_relaxed)));
   if (direct && a.n <= prismdb::dev::kDirectMaxSpans &&
@@ -706,6 +719,7 @@ int RunBatch(DeviceCtx& ctx, const SpanBatch& base_args, bool desc, bool verify,
     if ((rc = SideStream(w)) != 0) return rc;
     e = hipEventRecord(w->fork, s);
     if (e == hipSuccess) e = hipStreamWaitEvent(w->side, w->fork, 0);
+    side_join.armed = e == hipSuccess;
     if (e == hipSuccess) e = prismdb::dev::launch_long_list(a, ws, w->side);
     if (e == hipSuccess) e = hipEventRecord(w->join, w->side);
     if (e != hipSuccess) return FailHip(e, "long-span list launch");
@@ -713,6 +727,7 @@ int RunBatch(DeviceCtx& ctx, const SpanBatch& base_args, bool desc, bool verify,
     e = prismdb::dev::launch_lane(a, verify, ctx.cus, s);
     if (e == hipSuccess) e = hipStreamWaitEvent(s, w->join, 0);
     if (e != hipSuccess) return FailHip(e, "lane kernel launch");
+    side_join.armed = false;
     a.idx = ws.list;
     a.n_dev = &ws.counters->nlist;
     if (a.out != nullptr) a.out = ws.qout;
@@ -752,6 +767,7 @@ int RunBatch(DeviceCtx& ctx, const SpanBatch& base_args, bool desc, bool verify,
   e = hipEventRecord(w->fork, s);
   if (e == hipSuccess) e = hipStreamWaitEvent(w->side, w->fork, 0);
   if (e != hipSuccess) return FailHip(e, "side stream fork");
+  side_join.armed = true;
   e = prismdb::dev::launch_span(a, verify, ctx.cus, s);
   if (e != hipSuccess) return FailHip(e, "span kernel launch");
   SpanBatch seg{};
@@ -768,6 +784,7 @@ int RunBatch(DeviceCtx& ctx, const SpanBatch& base_args, bool desc, bool verify,
   if (e == hipSuccess) e = hipEventRecord(w->join, w->side);
   if (e == hipSuccess) e = hipStreamWaitEvent(s, w->join, 0);
   if (e != hipSuccess) return FailHip(e, "segment kernel launch");
+  side_join.armed = false;
   e = prismdb::dev::launch_combine(a, desc, verify, ws, s);
   if (e != hipSuccess) return FailHip(e, "combine kernel launch");
   if (lane) {
@@ -1033,6 +1050,23 @@ int prismdb_crc32c_last_schedule(uint64_t out[3]) {
   out[0] = c.tasks;
   out[1] = c.nslices;
   out[2] = t_last_pair ? 1u : 0u;
+  return 0;
+}
+
+// Test hook: the claimed tails of this thread's last planner-path batch:
+// out[0] = claims on the span / pair-run kernel's counter (slices or runs
+// taken on demand past the static deal, plus one failed claim per stream at
+// the end; 0 when the batch was too small for a tail), out[1] = the same for
+// the lane kernel's runs.  -2 after a one-launch batch, -1 before any.
+int prismdb_crc32c_last_claims(uint64_t out[2]) {
+  if (t_last_direct) return -2;
+  if (t_last_counters == nullptr || LastBatchStale()) return -1;
+  prismdb::dev::SplitCounters c{};
+  hipError_t e = hipStreamSynchronize(t_last_stream);
+  if (e == hipSuccess) e = hipMemcpy(&c, t_last_counters, sizeof(c), hipMemcpyDeviceToHost);
+  if (e != hipSuccess) return FailHip(e, "prismdb_crc32c_last_claims");
+  out[0] = c.claim;
+  out[1] = c.lane_claim;
   return 0;
 }
 

@@ -230,12 +230,15 @@ __global__ __launch_bounds__(kDirectThreads) void crc32c_direct_kernel(SpanBatch
     // first -- a file-sized call's waves 0-3 / 4-7 / 8-11 drained at 11.5 /
     // 12.3 / 13.4 us with the same six spans each (tools/direct_timeline.py,
     // profiles/r05/r05b_timeline_groups.json).  Group g's spans stay
-    // consecutive; unweighted when the groups are not all whole or a run
-    // would pass 64 spans.
+    // consecutive; unweighted when the groups are not all whole, a run
+    // would pass 64 spans, or the waves get fewer than 4 spans each (then
+    // 8:7:6 rounds to 2/1/0-span runs, and a two-span wave is the critical
+    // path while another idles; the weights were measured on file-sized
+    // calls, ~6 spans per wave).
     constexpr uint32_t kW0 = kRunWeight[0], kW1 = kRunWeight[1], kW2 = kRunWeight[2];
     constexpr uint32_t kWg = 4u * (kW0 + kW1 + kW2), kWmax = kW0 > kW1 ? (kW0 > kW2 ? kW0 : kW2) : (kW1 > kW2 ? kW1 : kW2);
     const uint64_t tot = (uint64_t)(K / kDirectWaves) * kWg;
-    if (K % kDirectWaves == 0u && (uint64_t)n * kWmax <= 63ull * tot) {
+    if (K % kDirectWaves == 0u && (uint64_t)n >= 4ull * K && (uint64_t)n * kWmax <= 63ull * tot) {
       const uint32_t g = wave / kDirectWaves, k = wave % kDirectWaves;
       const uint32_t wk = k < 4u ? kW0 : (k < 8u ? kW1 : kW2);
       const uint32_t cum = k < 4u ? k * kW0 : (k < 8u ? 4u * kW0 + (k - 4u) * kW1 : 4u * (kW0 + kW1) + (k - 8u) * kW2);

@@ -19,6 +19,9 @@
 // allocated between calls (each ~256 MiB pinned + ~256 MiB device).
 #include <hip/hip_runtime.h>
 
+#include <fcntl.h>
+#include <unistd.h>
+
 #include <algorithm>
 #include <atomic>
 #include <cstdlib>
@@ -232,6 +235,30 @@ void ParallelCopy(uint8_t* dst, const uint8_t* src, size_t bytes) {
   for (std::thread& x : th) x.join();
 }
 
+// True if the k bytes at p can be read and written by this process, checked
+// without touching them from user code: the kernel copies them into a pipe
+// and back (EFAULT instead of a fault on an unmapped or read-only page).  The
+// bytes end up unchanged.  Sealing probes its first and last trailer slots
+// with it, so that a read-only mapping (a file mmap'ed PROT_READ, an immutable
+// Python bytes object) is refused with EINVAL rather than crashing in the
+// trailer stores; the buffer TableBuilder seals is its writable heap append
+// buffer (util/env_posix.cc:279-309).
+bool HostWritable(uint8_t* p, size_t k) {
+  int fd[2];
+  if (pipe2(fd, O_CLOEXEC) != 0) return true;  // (cannot tell: leave it to the stores)
+  bool ok = write(fd[1], p, k) == (ssize_t)k;
+  if (ok) {
+    ok = read(fd[0], p, k) == (ssize_t)k;
+    if (!ok) {
+      uint8_t sink[8];
+      (void)!read(fd[0], sink, k);
+    }
+  }
+  close(fd[0]);
+  close(fd[1]);
+  return ok;
+}
+
 }  // namespace
 
 extern "C" {
@@ -258,6 +285,14 @@ int leveldb_crc32c_batch_host(const void* host_base, const uint64_t* off, const 
     if (i && off[i] < off[i - 1]) return PipeFail(PRISMDB_CRC32C_EINVAL, "spans must be sorted by offset");
     if (off[i] < lead || (seal && hdr && off[i] < 6))
       return PipeFail(PRISMDB_CRC32C_EINVAL, "log record header before the buffer start");
+  }
+  if (seal) {  // the signature's const does not hold under WRITE_TRAILER
+    uint8_t* const b = static_cast<uint8_t*>(const_cast<void*>(host_base));
+    for (size_t i : {(size_t)0, n - 1}) {
+      uint8_t* const t = hdr ? b + off[i] - 6 : b + off[i] + len[i];
+      if (!HostWritable(t, 4))
+        return PipeFail(PRISMDB_CRC32C_EINVAL, "WRITE_TRAILER: the host buffer is not writable at a trailer slot");
+    }
   }
   RingLease lease;
   int rc = lease.Acquire();

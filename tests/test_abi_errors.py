@@ -138,6 +138,56 @@ def test_python_host_batch_bounds(native):
         crc32c.batch_host(data, off, np.array([10, 10], dtype=np.uint32), init=np.array([1], dtype=np.uint32))
 
 
+def test_host_seal_rejects_read_only_memory(native):
+    """WRITE_TRAILER into a PROT_READ mapping returns EINVAL (the C side probes
+    the first and last trailer slots before the call stores anything) instead
+    of faulting in the trailer stores; the same spans without WRITE_TRAILER
+    get past that check (and, without a device, fail with EDEVICE)."""
+    import mmap
+
+    import torch
+
+    m = mmap.mmap(-1, 3 * 4096, prot=mmap.PROT_READ)
+    ro = np.frombuffer(m, dtype=np.uint8)
+    addr = ro.ctypes.data
+    off = np.array([0, 4096], dtype=np.uint64)
+    ln = np.array([4000, 4000], dtype=np.uint32)
+    out = np.zeros(2, dtype=np.uint32)
+    for flags in (WRITE_TRAILER | 1, WRITE_TRAILER | LOG_HEADER):
+        o = off + 8 if flags & LOG_HEADER else off
+        rc = native.leveldb_crc32c_batch_host(addr, o.ctypes.data, ln.ctypes.data, None, 2, out.ctypes.data,
+                                              None, flags)
+        assert rc == EINVAL and "not writable" in _err(native), (flags, rc, _err(native))
+    # writable memory passes the probe, and the probe leaves its bytes as they were
+    rw = np.arange(3 * 4096, dtype=np.uint64).astype(np.uint8)
+    before = rw.copy()
+    rc = native.leveldb_crc32c_batch_host(rw.ctypes.data, off.ctypes.data, ln.ctypes.data, None, 2,
+                                          out.ctypes.data, None, WRITE_TRAILER)
+    if not torch.cuda.is_available():
+        assert rc == EDEVICE, (rc, _err(native))
+        np.testing.assert_array_equal(rw, before)
+    del ro
+    m.close()
+
+
+def test_python_host_seal_rejects_read_only_or_strided(native):
+    """prismdb_amd.crc32c.batch_host: trailer=True on a read-only array (a
+    np.frombuffer view of bytes) or any call on a strided view raises
+    ValueError before the engine is called."""
+    from prismdb_amd import crc32c
+
+    off = np.array([0, 4096], dtype=np.uint64)
+    ln = np.array([4000, 4000], dtype=np.uint32)
+    ro = np.frombuffer(bytes(8192), dtype=np.uint8)
+    with pytest.raises(ValueError, match="read-only"):
+        crc32c.batch_host(ro, off, ln, mask=True, trailer=True)
+    strided = np.zeros(2 * 8192, dtype=np.uint8)[::2]
+    with pytest.raises(ValueError, match="contiguous"):
+        crc32c.batch_host(strided, off, ln)
+    with pytest.raises(ValueError, match="contiguous"):
+        crc32c.batch_host(strided, off, ln, trailer=True)
+
+
 def test_python_host_batch_offsets_do_not_wrap(native):
     """A negative offset (-1 would wrap to 2^64 - 1) and an offset past the
     buffer whose end wraps back inside it are rejected, not passed on."""

@@ -217,6 +217,110 @@ def test_multi_timing_diagnostics(devices, oracle):
     assert crc32c.multi_timing([devices[0], 63]) is None
 
 
+@pytest.fixture
+def self_gather(native):
+    """prismdb_crc32c_multi_self_gather on: partition 0 is enqueued by a
+    worker thread and its results reach out0 through the grouped
+    ncclSend / ncclRecv to itself."""
+    prev = native.prismdb_crc32c_multi_self_gather(1)
+    assert native.prismdb_crc32c_multi_self_gather(1) == 1, "test hooks are off"
+    yield
+    native.prismdb_crc32c_multi_self_gather(prev)
+
+
+@pytest.mark.parametrize("long_every", [0, 61])
+def test_multi_self_gather_one_device(devices, oracle, native, self_gather, long_every):
+    """The gather's RCCL call sequence on a one-device clique: partition 0's
+    batch enqueued by its worker thread into clique scratch, then grouped
+    ncclSend / ncclRecv of the 4-byte results and of the verify flags to
+    itself (comm, stream and counts as for a partition p > 0).  Seal, verify
+    and damaged verify, each bit-exact against the oracle; 20 calls back to
+    back through the same worker; the host timing diagnostics after them."""
+    import torch
+    from prismdb_amd import crc32c
+
+    host, off, lens = _partition(oracle, 0x5EED0350 + long_every, 30000, long_every)
+    want, _ = oracle.batch(host, off, lens, mask=True)
+    raw, _ = oracle.batch(host, off, lens)
+    dev = torch.device("cuda", devices[0])
+    buf, d_off, d_len = _to(dev, host, off, lens)
+    out = torch.full((len(off) + 5,), 0x3C3C3C3C, dtype=torch.int32, device=dev)
+    crc32c.batch_multi([(buf, d_off, d_len)], mask=True, trailer=True, out=out)
+    got = _u32(out)
+    np.testing.assert_array_equal(got[:len(off)], want)
+    assert (got[len(off):] == 0x3C3C3C3C).all()  # nothing past the partition's results
+    outs = [torch.empty(len(off), dtype=torch.int32, device=dev) for _ in range(20)]
+    mms = [torch.full((len(off),), 9, dtype=torch.uint8, device=dev) for _ in range(20)]
+    for o, m in zip(outs, mms):
+        crc32c.batch_multi([(buf, d_off, d_len)], verify=True, out=o, mismatch=m, check_bounds=False)
+    torch.cuda.synchronize()
+    for o, m in zip(outs, mms):
+        np.testing.assert_array_equal(_u32(o), raw)
+        assert not m.cpu().numpy().any()
+    ht = crc32c.multi_host_timing([devices[0]])
+    assert ht is not None and ht["enqueue_us"][0] > 0 and ht["call_us"] >= ht["enqueue_us"][0]
+    bad = [5, len(off) // 2, len(off) - 1]
+    for i in bad:
+        buf[int(off[i]) + 3] ^= 0x08
+    out, mm = crc32c.batch_multi([(buf, d_off, d_len)], verify=True)
+    assert sorted(np.flatnonzero(mm.cpu().numpy()).tolist()) == bad
+
+
+def test_multi_self_gather_failure_hands_back(devices, oracle, native, self_gather):
+    """Under the self-gather hook, an injected failure after partition 0's
+    batch (enqueued by its worker): the call raises with the worker's
+    message on the calling thread, the caller's stream still waits for the
+    batch, and the next call gathers its own results."""
+    import torch
+    from prismdb_amd import crc32c
+    from prismdb_amd._lib import NativeLibraryError
+
+    dev = torch.device("cuda", devices[0])
+    host, off, lens = _partition(oracle, 0x5EED0360, 20000, 0)
+    want, _ = oracle.batch(host, off, lens)
+    buf, d_off, d_len = _to(dev, host, off, lens)
+    out = torch.zeros(len(off), dtype=torch.int32, device=dev)
+    prev = native.prismdb_crc32c_multi_fail_after(0)
+    try:
+        with pytest.raises(NativeLibraryError, match="injected failure"):
+            crc32c.batch_multi([(buf, d_off, d_len)], out=out, check_bounds=False)
+        out.fill_(0x5A5A5A5A)
+    finally:
+        native.prismdb_crc32c_multi_fail_after(prev)
+    torch.cuda.synchronize()
+    assert bool((out == 0x5A5A5A5A).all())
+    out2, _ = crc32c.batch_multi([(buf, d_off, d_len)], check_bounds=False)
+    np.testing.assert_array_equal(_u32(out2), want)
+
+
+def test_multi_host_enqueue_timing(devices, oracle):
+    """prismdb_crc32c_multi_host_timing after a config-5-shaped planner-path
+    call (> 2^18 spans): partition 0's enqueue time and start offset, and
+    the whole call's host time; the enqueue is a small fraction of the
+    device batch (the skew bound the workers exist for)."""
+    import torch
+    from prismdb_amd import crc32c
+
+    dev = torch.device("cuda", devices[0])
+    nb = 300_000
+    off = np.arange(nb, dtype=np.uint64) * 3992 + 8
+    lens = np.full(nb, 3988, dtype=np.uint32)
+    buf = torch.empty(int(off[-1]) + 4096, dtype=torch.uint8, device=dev)
+    crc32c.fill_synthetic(buf, 0x5EED0370)
+    d_off = torch.from_numpy(off.astype(np.int64)).to(dev)
+    d_len = torch.from_numpy(lens.view(np.int32)).to(dev)
+    out = torch.empty(nb, dtype=torch.int32, device=dev)
+    for _ in range(3):
+        crc32c.batch_multi([(buf, d_off, d_len)], mask=True, trailer=True, out=out, check_bounds=False)
+    torch.cuda.synchronize()
+    ht = crc32c.multi_host_timing([devices[0]])
+    tm = crc32c.multi_timing([devices[0]])
+    assert ht is not None and tm is not None
+    assert 0 < ht["enqueue_us"][0] < 1e3 * tm["batch_ms"][0]
+    assert ht["start_us"][0] >= 0 and ht["call_us"] >= ht["enqueue_us"][0]
+    print("host enqueue us", ht, "device batch ms", tm["batch_ms"])
+
+
 def test_multi_rejects_bad_outputs(devices):
     """out / mismatch shorter than the partitions' total, of the wrong dtype
     or not on the root device are rejected before the C ABI writes them."""

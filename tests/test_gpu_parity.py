@@ -1065,8 +1065,11 @@ def test_lane_claimed_tail_runs(dev, oracle, native):
     from conftest import set_route
     from prismdb_amd import crc32c
 
+    import torch as _t
+
     rng = np.random.default_rng(0x5EED0070)
-    n = 1_600_000
+    cus = _t.cuda.get_device_properties(0).multi_processor_count
+    n = max(1_600_000, 64 * 11 * 8 * cus)  # > (kLaneTailRounds + 2) runs per wave (8 waves per CU)
     lens = rng.integers(8, 200, size=n).astype(np.uint64)
     lens[rng.integers(0, n, size=300)] = rng.integers(1281, 4000, size=300).astype(np.uint64)
     gaps = rng.integers(7, 20, size=n).astype(np.uint64)
@@ -1087,11 +1090,87 @@ def test_lane_claimed_tail_runs(dev, oracle, native):
     restore = set_route(native, "lane_log")
     try:
         out, mm = crc32c.batch(buf, d_off, d_len, mask=True, verify=True, log_header=True)
+        claims = _last_claims(native)
     finally:
         restore()
     np.testing.assert_array_equal(_u32(out), want)
     np.testing.assert_array_equal(mm.cpu().numpy(), damaged.astype(np.uint8))
     assert oracle.mask(int(raw[0])) == int(masked[0] ^ damaged[0])
+    assert claims[1] > 0, "the lane kernel's tail was never claimed"
+
+
+def _last_claims(native):
+    """{span / pair-run kernel claims, lane kernel claims} of this thread's
+    last planner-path batch (test hook prismdb_crc32c_last_claims)."""
+    arr = (ctypes.c_uint64 * 2)()
+    assert native.prismdb_crc32c_last_claims(arr) == 0
+    return list(arr)
+
+
+@pytest.mark.parametrize("kernel", ["pair", "span"])
+def test_claimed_tails_engage(dev, oracle, native, kernel):
+    """Batches sized from the device's CU count so that the planner kernels'
+    claimed tails engage: the pair-run kernel (one-task spans, >= 16 pairs
+    per run: 64 B spans, ~2300 per wave) and the span kernel (task-balanced
+    slices of >= 32 tasks, 16 per stream: spans of 1-3 chunks, ~16 GiB).
+    The claim counter read back is > 0, and the results are bit-exact: every
+    span for the pair batch, a sample plus the ends (host-regenerated bytes)
+    for the span batch."""
+    import torch
+    from prismdb_amd import crc32c
+
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    nwaves = 16 * cus  # kWavesPerGroup, one group per CU
+    seed = 0x5EED0080 + (kernel == "span")
+    if kernel == "pair":
+        n = 2300 * nwaves  # np / (64 nwaves) ~ 18 pairs per run >= 16
+        off = np.arange(n, dtype=np.uint64) * 64 + 3
+        lens = np.full(n, 61, dtype=np.uint32)
+        host = oracle.synth(n * 64 + 64, seed)
+        buf = torch.from_numpy(host).to(dev)
+    else:
+        rng = np.random.default_rng(seed)
+        streams = 2 * nwaves
+        tasks_per_span = rng.integers(1, 4, size=int(600 * streams / 2)).astype(np.uint64)  # ~600 tasks per stream
+        lens = (tasks_per_span * 4096 - rng.integers(0, 300, size=len(tasks_per_span)).astype(np.uint64)).astype(np.uint32)
+        n = len(lens)
+        off = np.cumsum(np.concatenate([[5], lens[:-1].astype(np.uint64) + 7])).astype(np.uint64)
+        total = int(off[-1]) + int(lens[-1]) + 64
+        free, _ = torch.cuda.mem_get_info()
+        if free < total + (4 << 30):
+            pytest.skip("not enough device memory")
+        buf = torch.empty(total, dtype=torch.uint8, device=dev)
+        crc32c.fill_synthetic(buf, seed)
+    d_off = torch.from_numpy(off.astype(np.int64)).to(dev)
+    d_len = torch.from_numpy(lens.view(np.int32)).to(dev)
+    restore = set_route_planner(native)
+    try:
+        out, _ = crc32c.batch(buf, d_off, d_len, mask=True, check_bounds=False)
+        sched = (ctypes.c_uint64 * 3)()
+        assert native.prismdb_crc32c_last_schedule(sched) == 0
+        claims = _last_claims(native)
+    finally:
+        restore()
+    got = _u32(out)
+    if kernel == "pair":
+        assert sched[1] == 0 and sched[2] == 1  # every record one task: the pair-run kernel's schedule
+        want, _ = oracle.batch(host, off, lens, mask=True)
+        np.testing.assert_array_equal(got, want)
+    else:
+        assert sched[1] > 0 and sched[0] // sched[1] >= 32, list(sched)  # task-balanced slices of >= 32 tasks
+        idx = np.unique(np.concatenate([[0, n - 1], np.random.default_rng(1).integers(0, n, 2048)]))
+        for i in idx.tolist():
+            blk = oracle.synth(int(lens[i]), seed, int(off[i]))
+            assert int(got[i]) == oracle.mask(oracle.value(blk.tobytes())), i
+    assert claims[0] > 0, f"the {kernel} kernel's tail was never claimed ({list(sched)})"
+    del buf, d_off, d_len, out
+    torch.cuda.empty_cache()
+
+
+def set_route_planner(native):
+    from conftest import set_route
+
+    return set_route(native, "span_only")
 
 
 @pytest.mark.parametrize("layout", ["runs", "all_long", "one_short_run", "under_a_run"])

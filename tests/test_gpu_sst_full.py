@@ -1,0 +1,202 @@
+"""A full-size table written by the reference itself, on the device.
+
+oracle/_ref/sst_fixture is the reference's TableBuilder -> Table::Open ->
+ReadBlock(verify_checksums) path compiled from /root/reference/table/*.cc by
+oracle/Makefile (test infrastructure; the binary travels with the tree, the
+reference sources do not).  Here it writes a 64 MiB-class table shaped like
+configs 4/5's compaction outputs -- 67 000 keys x 980-byte values, 4 KiB
+blocks, kNoCompression: ~16 750 data blocks of ~3 960 B, a metaindex block and
+a ~470 KiB index block, each followed by its 5-byte trailer
+(table/table_builder.cc:94-131,185-261) -- and re-reads it with checksum
+verification before it is handed over.  Its JSON lists every block's handle
+and stored masked crc.  Against that file:
+
+  * sst.verify_tables flags nothing on the clean file and exactly the
+    damaged blocks after flips in data blocks and in stored trailers
+    (ReadBlock, table/format.cc:66-102), the whole file in one call;
+  * sst.seal_blocks over the file with its 4 crc bytes zeroed reproduces the
+    reference's file byte for byte (WriteRawBlock);
+  * 7 and 12 copies per call -- the one-launch kernel (<= 2^17 spans), its
+    windows and the planner path (> 2^17) -- sealed and verified.
+
+Skipped when oracle/_ref/sst_fixture was not built (no /root/reference where
+the tree was built)."""
+import ctypes
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+FIXTURE = os.path.join(ROOT, "oracle", "_ref", "sst_fixture")
+NKEYS, VLEN, BLOCK = 67000, 980, 4096
+
+
+@pytest.fixture(scope="module")
+def table(tmp_path_factory):
+    if not os.path.exists(FIXTURE):
+        pytest.skip("oracle/_ref/sst_fixture not built (needs /root/reference at build time)")
+    d = tmp_path_factory.mktemp("sst_full")
+    ldb, js = str(d / "full.ldb"), str(d / "full.json")
+    subprocess.run([FIXTURE, ldb, js, str(NKEYS), str(VLEN), str(BLOCK)], check=True, capture_output=True,
+                   timeout=120)
+    with open(ldb, "rb") as f:
+        img = f.read()
+    with open(js) as f:
+        meta = json.load(f)
+    assert meta["file_size"] == len(img) and len(img) > 60 << 20
+    return img, meta
+
+
+@pytest.fixture(scope="module")
+def dev(native):
+    import torch
+
+    assert torch.cuda.is_available(), "gpu tests need a HIP device"
+    from prismdb_amd import crc32c
+
+    crc32c.device_init(0)
+    return torch.device("cuda", 0)
+
+
+def _spans(img, meta):
+    """The walker's spans (contents || type) and the fixture's list agree."""
+    from prismdb_amd import sst
+
+    off, ln, kind = sst.block_spans(img)
+    blocks = meta["blocks"]
+    got = sorted(zip(off.tolist(), (ln - 1).tolist()))
+    want = sorted((b["offset"], b["size"]) for b in blocks)
+    assert got == want
+    return off, ln, kind
+
+
+def _last_split_rc(native):
+    arr = (ctypes.c_uint64 * 4)()
+    return native.prismdb_crc32c_last_split(arr)
+
+
+def test_full_sst_shape(table):
+    """The table has the configs 4/5 geometry the bench assumes."""
+    img, meta = table
+    kinds = [b["kind"] for b in meta["blocks"]]
+    data = [b["size"] for b in meta["blocks"] if b["kind"] == "data"]
+    index = [b["size"] for b in meta["blocks"] if b["kind"] == "index"]
+    assert kinds.count("data") > 16000 and kinds.count("index") == 1 and kinds.count("metaindex") == 1
+    assert 3900 < np.median(data) < 4096 and index[0] > 300_000
+
+
+def test_full_sst_verify_clean_and_damaged(dev, native, table):
+    """One file, one call (the one-launch kernel, the index block through its
+    tickets): clean -> nothing flagged; then flips in two data blocks, in the
+    index block's stored crc and in a data block's stored crc -> exactly those
+    four flagged, every other block OK."""
+    from prismdb_amd import sst
+
+    img, meta = table
+    off, ln, kind = _spans(img, meta)
+    res = sst.verify_tables([img])
+    assert res.ok and len(res.blocks) == len(off)
+    assert _last_split_rc(native) == -2  # one launch of the one-launch kernel
+    bad = bytearray(img)
+    blocks = meta["blocks"]
+    data_idx = [i for i, b in enumerate(blocks) if b["kind"] == "data"]
+    index_i = next(i for i, b in enumerate(blocks) if b["kind"] == "index")
+    v_data = [data_idx[7], data_idx[-1]]
+    v_crc = [index_i, data_idx[len(data_idx) // 2]]
+    for i in v_data:
+        bad[blocks[i]["offset"] + blocks[i]["size"] // 2] ^= 0x04
+    for i in v_crc:
+        bad[blocks[i]["offset"] + blocks[i]["size"] + 2] ^= 0x10  # the stored crc (after the type byte)
+    res = sst.verify_tables([bytes(bad)])
+    flagged = sorted(b.offset for b in res.bad_blocks())
+    assert flagged == sorted(blocks[i]["offset"] for i in v_data + v_crc)
+    assert not any(res.table_errors)
+
+
+def test_full_sst_seal_reproduces_file(dev, native, table):
+    """WriteRawBlock over the whole file: the 4 crc bytes of every trailer
+    zeroed (the type byte kept), one sealing call -> the reference's file
+    byte for byte, and the results equal the fixture's masked crcs."""
+    import torch
+    from prismdb_amd import sst
+
+    img, meta = table
+    off, ln, _ = _spans(img, meta)
+    host = np.frombuffer(img, dtype=np.uint8).copy()
+    crc_at = (off + ln.astype(np.uint64)).astype(np.int64)[:, None] + np.arange(4)[None, :]
+    host[crc_at] = 0
+    buf = torch.from_numpy(host).to(dev)
+    d_off = torch.from_numpy(off.astype(np.int64)).to(dev)
+    d_size = torch.from_numpy((ln - 1).view(np.int32)).to(dev)
+    out = sst.seal_blocks(buf, d_off, d_size)
+    assert _last_split_rc(native) == -2
+    want = {b["offset"]: b["masked_crc"] for b in meta["blocks"]}
+    got = out.cpu().numpy().view(np.uint32)
+    assert all(int(got[i]) == want[int(o)] for i, o in enumerate(off.tolist()))
+    assert buf.cpu().numpy().tobytes() == img
+
+
+@pytest.mark.parametrize("copies,route", [(7, "direct"), (12, "windows"), (12, "planner")])
+def test_full_sst_copies_per_call(dev, native, table, copies, route):
+    """A compaction's worth of reference tables per call: `copies` copies of
+    the file back to back (16-B aligned), sealed from zeroed crcs in one call
+    (byte-identical to the copies of the reference file), then verified in
+    one call with one damaged data block per copy (exactly those flagged).
+    7 copies take one launch of the one-launch kernel; 12 copies (~201 K
+    spans) take its windows (the default up to 2^18 spans) or, pinned, the
+    planner path."""
+    import torch
+    from prismdb_amd import crc32c
+
+    img, meta = table
+    off1, ln1, _ = _spans(img, meta)
+    fb = (len(img) + 15) & ~15
+    orig = np.zeros(copies * fb, dtype=np.uint8)
+    src = np.frombuffer(img, dtype=np.uint8)
+    for c in range(copies):
+        orig[c * fb:c * fb + len(img)] = src
+    off = (np.arange(copies, dtype=np.uint64)[:, None] * np.uint64(fb) + off1[None, :]).reshape(-1)
+    ln = np.tile(ln1, copies)
+    n = len(off)
+    crc_at = (off + ln.astype(np.uint64)).astype(np.int64)[:, None] + np.arange(4)[None, :]
+    zeroed = orig.copy()
+    zeroed[crc_at] = 0
+    buf = torch.from_numpy(zeroed).to(dev)
+    d_off = torch.from_numpy(off.astype(np.int64)).to(dev)
+    d_len = torch.from_numpy(ln.view(np.int32)).to(dev)
+    prev = native.prismdb_crc32c_windows(0 if route == "planner" else 2)
+    try:
+        out, _ = crc32c.batch(buf, d_off, d_len, mask=True, trailer=True, check_bounds=False)
+        sealed_route = _last_split_rc(native)
+        masked = out.cpu().numpy().view(np.uint32).copy()
+        np.testing.assert_array_equal(buf.cpu().numpy(), orig)
+        rng = np.random.default_rng(copies)
+        victims = []
+        for c in range(copies):
+            i = c * len(off1) + int(rng.integers(0, len(off1) - 3))
+            victims.append(i)
+            buf[int(off[i]) + 11] ^= 0x20
+        out2, mm = crc32c.batch(buf, d_off, d_len, verify=True, check_bounds=False)
+        verify_route = _last_split_rc(native)
+    finally:
+        native.prismdb_crc32c_windows(prev)
+    assert sorted(np.flatnonzero(mm.cpu().numpy()).tolist()) == sorted(victims)
+    want = np.tile(np.array([b["masked_crc"] for b in sorted(meta["blocks"], key=lambda b: b["offset"])],
+                            dtype=np.uint32), copies)
+    order = np.tile(np.argsort(np.argsort(off1)), copies) + np.repeat(np.arange(copies) * len(off1), len(off1))
+    np.testing.assert_array_equal(masked, want[order])
+    raw = out2.cpu().numpy().view(np.uint32)
+    clean = np.ones(n, dtype=bool)
+    clean[victims] = False
+    unmasked = np.array([crc32c.Unmask(int(x)) for x in masked[clean][:4096]], dtype=np.uint32)
+    np.testing.assert_array_equal(raw[clean][:4096], unmasked)
+    if route == "planner":
+        assert sealed_route == 0 and verify_route == 0  # the planner path ran (not the one-launch kernel)
+    else:
+        assert sealed_route == -2 and verify_route == -2
+    assert n == copies * len(off1)

@@ -35,6 +35,7 @@ extern "C" {
 uint32_t prismdb_crc32c_extend_portable(uint32_t init_crc, const char* data, size_t n);
 void prismdb_crc32c_force_generic(int on);
 uint64_t prismdb_crc32c_direct_max(uint64_t n);
+int prismdb_test_hooks_enabled(void);
 }
 
 #define CHECK(c)                                                              \
@@ -264,6 +265,10 @@ int RunAbi(bool expect_no_device) {
 }
 
 int RunThreads(int nthreads, int iters, const char* sst) {
+  // the setters below store only with the test hooks on (read once, at the
+  // first hook call): without this the run would race nothing
+  setenv("PRISMDB_ENABLE_TEST_HOOKS", "1", 1);
+  CHECK(prismdb_test_hooks_enabled() == 1);
   const std::vector<uint8_t> img = ReadFile(sst);
   std::atomic<int> failures{0};
   std::vector<std::thread> ts;
