@@ -282,6 +282,12 @@ struct Workspace {
   size_t cap_s = 0;
   char* direct = nullptr;  // word, done | ticket map | partials | per-span counters
   uint32_t gen = 0;
+  // Planner calls alternate between two counter blocks (pcall parity); each
+  // call's plan kernel zeroes the block of the next.  dirty: a call used its
+  // block and failed before its plan kernel was enqueued, so the next call
+  // fills its block first.
+  uint32_t pcall = 0;
+  bool dirty = false;
   bool owned = false;  // an engine stream's (g_owned), not a thread's
   SplitWs ws{};
 };
@@ -295,7 +301,11 @@ constexpr size_t kMaxWorkspaces = 8;
 // device-wide), free every block on the device's release stream, and trim
 // the default pool so the memory leaves the process's pool too.
 void SyncAndRelease(Workspace& w) {
-  if (t_last_counters == w.ws.counters) t_last_counters = nullptr;
+  {
+    const char* t = reinterpret_cast<const char*>(t_last_counters);
+    const char* c = reinterpret_cast<const char*>(w.ws.counters);
+    if (c != nullptr && t >= c && t < c + 512) t_last_counters = nullptr;
+  }
   if (w.direct != nullptr && t_last_stats == reinterpret_cast<const uint32_t*>(w.direct + 32)) t_last_stats = nullptr;
   int cur = 0;
   (void)hipGetDevice(&cur);
@@ -371,11 +381,13 @@ int InitWorkspace(Workspace& w, int device, hipStream_t s) {
   w.device = device;
   w.stream = s;
   hipError_t e = hipSuccess;
-  const size_t bytes = 256 + kCapSeg * (16 + 4) + (size_t)kCapLong * (8 + 8 + 4) +
+  const size_t bytes = 512 + kCapSeg * (16 + 4) + (size_t)kCapLong * (8 + 8 + 4) +
                        (size_t)prismdb::dev::kMaxPlanBlocks * 8;
   e = hipEventCreateWithFlags(&w.done[0], hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&w.done[1], hipEventDisableTiming);
   if (e == hipSuccess) e = hipMallocAsync(&w.mem, bytes, s);
+  // both planner counter blocks start zeroed (then each call zeroes the next's)
+  if (e == hipSuccess) e = hipMemsetAsync(w.mem, 0, 512, s);
   if (e != hipSuccess) {
     for (hipEvent_t ev : w.done)
       if (ev != nullptr) (void)hipEventDestroy(ev);
@@ -383,8 +395,8 @@ int InitWorkspace(Workspace& w, int device, hipStream_t s) {
     return FailHip(e, "workspace allocation");
   }
   char* p = static_cast<char*>(w.mem);
-  w.ws.counters = reinterpret_cast<SplitCounters*>(p);
-  p += 256;
+  w.ws.counters = reinterpret_cast<SplitCounters*>(p);  // two 256-B blocks, one per call parity
+  p += 512;
   w.ws.seg_rec = reinterpret_cast<prismdb::dev::SpanRec*>(p);
   p += kCapSeg * 16;
   w.ws.long_span = reinterpret_cast<uint64_t*>(p);
@@ -681,10 +693,22 @@ int RunBatch(DeviceCtx& ctx, const SpanBatch& base_args, bool desc, bool verify,
   // its kernels are in git history: crc32c_kernels.hip at 36498f1.)
   const uint32_t streams = 2u * (uint32_t)ctx.cus * prismdb::dev::kWavesPerGroup;
   if ((rc = PlannerWorkspace(*w, s, a.n, streams, lane, &ws)) != 0) return rc;
-  // (the whole 256-B counter block: one fill kernel; 56 bytes took two)
-  static_assert(sizeof(SplitCounters) <= 256, "the workspace reserves 256 B for the counters");
-  hipError_t e = hipMemsetAsync(ws.counters, 0, 256, s);
-  if (e != hipSuccess) return FailHip(e, "hipMemsetAsync");
+  // Counters: the block of this call's parity, zeroed by the previous
+  // planner call's plan kernel (or at the workspace's creation) -- no fill
+  // kernel in front of the call (it and its gap took 6.7 us of a config-5
+  // call, profiles/r05/r05aa_c5_seal/one_call_timeline.csv).
+  static_assert(sizeof(SplitCounters) <= 256, "each call parity's counter block is 256 B");
+  {
+    char* const cb = reinterpret_cast<char*>(w->ws.counters);
+    ws.counters = reinterpret_cast<SplitCounters*>(cb + 256u * (w->pcall & 1u));
+    ws.zero_next = reinterpret_cast<SplitCounters*>(cb + 256u * ((w->pcall + 1u) & 1u));
+  }
+  hipError_t e = hipSuccess;
+  if (w->dirty) {  // the last call failed after using this block, before its plan kernel
+    e = hipMemsetAsync(ws.counters, 0, 256, s);
+    if (e != hipSuccess) return FailHip(e, "hipMemsetAsync");
+  }
+  w->dirty = true;  // until this call's plan kernel is enqueued
   t_last_counters = ws.counters;
   t_last_stream = s;
   t_last_direct = false;
@@ -738,13 +762,24 @@ int RunBatch(DeviceCtx& ctx, const SpanBatch& base_args, bool desc, bool verify,
   a.chunk_lg = (a.flags & prismdb::dev::kFlagLogHeader) ? prismdb::dev::kLgChunkWordsLog : 10u;
   a.overflow = &ws.counters->overflow;
   a.rec = ws.rec;
-  e = prismdb::dev::launch_plan(a, desc, ws, s);
-  if (e != hipSuccess) return FailHip(e, "plan kernel launch");
+  // The segment pass (long spans' 32 KiB pieces) needs only the plan: it
+  // runs on the workspace's side stream next to the span kernel, and takes
+  // CUs as the span kernel's groups leave them (~100 us of an SST-descriptor
+  // call ran after it before).  The combine waits for both.  The fork is the
+  // stop event of the last kernel before the span kernel (the slice mark, or
+  // the plan), not a marker after it: a marker there held the span kernel
+  // back ~6.5 us (profiles/r05/r05aa_c5_seal/one_call_timeline.csv).
+  if ((rc = SideStream(w)) != 0) return rc;
   // Task-balanced slices need more records than span streams: with n <= the
   // stream count every stream holds at most one record either way, and the
   // two slice kernels' launches are ~9 us of a file-sized call.
-  if (a.n > streams) {
-    e = prismdb::dev::launch_slices(a, ws, s);
+  const bool sliced = a.n > streams;
+  e = prismdb::dev::launch_plan(a, desc, ws, s, sliced ? nullptr : w->fork);
+  if (e != hipSuccess) return FailHip(e, "plan kernel launch");
+  w->pcall++;  // the next call's block is the one this plan kernel zeroes
+  w->dirty = false;
+  if (sliced) {
+    e = prismdb::dev::launch_slices(a, ws, s, w->fork);
     if (e != hipSuccess) return FailHip(e, "slice kernels launch");
     a.slice_start = ws.slice_start;
     a.nslices_dev = &ws.counters->nslices;
@@ -759,13 +794,7 @@ int RunBatch(DeviceCtx& ctx, const SpanBatch& base_args, bool desc, bool verify,
                       : 0u;
   t_last_pair = a.pair_kernel != 0u;
   a.claim = &ws.counters->claim;  // (zeroed with the counters above)
-  // The segment pass (long spans' 32 KiB pieces) needs only the plan: it
-  // runs on the workspace's side stream next to the span kernel, and takes
-  // CUs as the span kernel's groups leave them (~100 us of an SST-descriptor
-  // call ran after it before).  The combine waits for both.
-  if ((rc = SideStream(w)) != 0) return rc;
-  e = hipEventRecord(w->fork, s);
-  if (e == hipSuccess) e = hipStreamWaitEvent(w->side, w->fork, 0);
+  e = hipStreamWaitEvent(w->side, w->fork, 0);
   if (e != hipSuccess) return FailHip(e, "side stream fork");
   side_join.armed = true;
   e = prismdb::dev::launch_span(a, verify, ctx.cus, s);
@@ -780,26 +809,29 @@ int RunBatch(DeviceCtx& ctx, const SpanBatch& base_args, bool desc, bool verify,
   seg.role = prismdb::dev::kRoleSegments;
   seg.tabs = ctx.tabs;
   seg.rec = ws.seg_rec;
-  e = prismdb::dev::launch_span(seg, false, ctx.cus, w->side);
-  if (e == hipSuccess) e = hipEventRecord(w->join, w->side);
+  e = prismdb::dev::launch_span(seg, false, ctx.cus, w->side, w->join);  // the join: its stop event
   if (e == hipSuccess) e = hipStreamWaitEvent(s, w->join, 0);
   if (e != hipSuccess) return FailHip(e, "segment kernel launch");
   side_join.armed = false;
-  e = prismdb::dev::launch_combine(a, desc, verify, ws, s);
+  // The call's last kernel completes the workspace's done event itself (its
+  // stop event) instead of a marker after it (MarkDone, on an error return).
+  hipEvent_t const done = w->done[w->gen & 1u];
+  e = prismdb::dev::launch_combine(a, desc, verify, ws, s, lane || trailer_pass ? nullptr : done);
   if (e != hipSuccess) return FailHip(e, "combine kernel launch");
   if (lane) {
     SpanBatch back = a;
     back.out = res_out;
     back.mismatch = caller_mm;
-    e = prismdb::dev::launch_scatter(back, ws, ws.qout, ws.qmm, s);
+    e = prismdb::dev::launch_scatter(back, ws, ws.qout, ws.qmm, s, trailer_pass ? nullptr : done);
     if (e != hipSuccess) return FailHip(e, "scatter kernel launch");
   }
   if (trailer_pass) {
     SpanBatch t = base_args;
     t.n = a.n;
-    e = prismdb::dev::launch_trailers(t, desc, res_out, s);
+    e = prismdb::dev::launch_trailers(t, desc, res_out, s, done);
     if (e != hipSuccess) return FailHip(e, "trailer kernel launch");
   }
+  mark.by_launch = true;
   return 0;
 }
 

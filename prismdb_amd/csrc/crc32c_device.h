@@ -124,6 +124,9 @@ struct SplitCounters {
 
 struct SplitWs {
   SplitCounters* counters;
+  // The other call parity's counter block: the plan kernel zeroes it for the
+  // workspace's next planner call (nullptr: none).
+  SplitCounters* zero_next;
   SpanRec* rec;      // one per span of the batch
   SpanRec* seg_rec;  // one per segment
   uint32_t* seg_out;
@@ -180,12 +183,12 @@ constexpr uint32_t kSlicesPerStream = 16;  // span kernel: task-balanced slices 
 constexpr uint64_t kMaxGenericSpans = 1ull << 30;  // per generic-path launch sequence
 constexpr uint32_t kPlanThreads = 256;
 
-hipError_t launch_span(const SpanBatch& a, bool verify, int grid, hipStream_t s);
+hipError_t launch_span(const SpanBatch& a, bool verify, int grid, hipStream_t s, hipEvent_t stop = nullptr);
 hipError_t launch_fixed(const SpanBatch& a, bool verify, int grid, hipStream_t s);
-hipError_t launch_plan(const SpanBatch& a, bool desc, const SplitWs& ws, hipStream_t s);
-hipError_t launch_slices(const SpanBatch& a, const SplitWs& ws, hipStream_t s);
+hipError_t launch_plan(const SpanBatch& a, bool desc, const SplitWs& ws, hipStream_t s, hipEvent_t stop = nullptr);
+hipError_t launch_slices(const SpanBatch& a, const SplitWs& ws, hipStream_t s, hipEvent_t stop = nullptr);
 hipError_t launch_combine(const SpanBatch& a, bool desc, bool verify, const SplitWs& ws,
-                          hipStream_t s);
+                          hipStream_t s, hipEvent_t stop = nullptr);
 hipError_t launch_long_list(const SpanBatch& a, const SplitWs& ws, hipStream_t s);
 hipError_t launch_lane(const SpanBatch& a, bool verify, int grid, hipStream_t s);
 constexpr int kListThreads = 1024;  // crc32c_long_list_kernel block: one atomic per 16 runs
@@ -195,10 +198,11 @@ constexpr int kListThreads = 1024;  // crc32c_long_list_kernel block: one atomic
 hipError_t launch_direct(const SpanBatch& a, bool verify, int grid, const DirectWs& d, hipStream_t s,
                          hipEvent_t done);
 hipError_t launch_scatter(const SpanBatch& a, const SplitWs& ws, const uint32_t* qout, const uint8_t* qmm,
-                          hipStream_t s);
+                          hipStream_t s, hipEvent_t stop = nullptr);
 // WRITE_TRAILER on the planner path: every span's trailer from res[i], after
 // the span kernels (crc32c_trailer_kernel).
-hipError_t launch_trailers(const SpanBatch& a, bool desc, const uint32_t* res, hipStream_t s);
+hipError_t launch_trailers(const SpanBatch& a, bool desc, const uint32_t* res, hipStream_t s,
+                           hipEvent_t stop = nullptr);
 
 }  // namespace dev
 }  // namespace prismdb

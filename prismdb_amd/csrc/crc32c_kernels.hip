@@ -37,6 +37,7 @@
 //                           padding rounds
 //   crc32c_pair_kernel<verify>  large batches of one-task records (pair runs)
 //   crc32c_combine_kernel   stitches segments back into long spans
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -937,6 +938,10 @@ __device__ __forceinline__ uint64_t batch_n(const SpanBatch& a) {
 
 template <bool kDesc>
 __global__ __launch_bounds__(kPlanThreads) void crc32c_plan_kernel(SpanBatch a, SplitWs ws) {
+  // the next call's counters (the other parity's block, idle since the call
+  // before this one): zeroed here instead of by a fill kernel in front of it
+  if (blockIdx.x == 0u && threadIdx.x < 64u && ws.zero_next != nullptr)
+    reinterpret_cast<uint32_t*>(ws.zero_next)[threadIdx.x] = 0u;
   const uint64_t n = batch_n(a);
   const uint64_t lo = (uint64_t)blockIdx.x * ws.tile;
   if (lo >= n) {  // (behind the lane kernel the list is often empty: ~4000 blocks leave at once)
@@ -1612,20 +1617,30 @@ __global__ __launch_bounds__(256) void crc32c_trailer_kernel(SpanBatch a, const 
 
 // ---------------------------------------------------------------------------
 // Host-side launchers (called from crc32c_capi.hip through crc32c_device.h).
+// `stop`, where a launcher takes one: an event completed by the kernel's own
+// end (hipExtLaunchKernel's stop event) instead of a marker packet after it --
+// the planner path's fork onto its side stream, its join and its done event
+// (a marker between two kernels cost ~2.7 us of the stream's time,
+// profiles/r06/r06f_percall_floor/floor.json direct_ts_plain).
 // ---------------------------------------------------------------------------
-hipError_t launch_span(const SpanBatch& a, bool verify, int grid, hipStream_t s) {
+template <typename... P, typename... A>
+hipError_t launch_k(void (*k)(P...), dim3 grid, dim3 block, hipStream_t s, hipEvent_t stop, A... args) {
+  if (stop != nullptr) hipExtLaunchKernelGGL(k, grid, block, 0, s, nullptr, stop, 0u, args...);
+  else hipLaunchKernelGGL(k, grid, block, 0, s, args...);
+  return hipGetLastError();
+}
+
+hipError_t launch_span(const SpanBatch& a, bool verify, int grid, hipStream_t s, hipEvent_t stop) {
   // Log records (LOG_HEADER) are short: the variant that skips padding rounds.
   const bool skip = (a.flags & kFlagLogHeader) != 0 && a.role == kRoleSpans;
   if (verify) {
     if (a.pair_kernel && !skip) crc32c_pair_kernel<true><<<grid, kThreads, 0, s>>>(a);
-    if (skip) crc32c_span_kernel<true, true><<<grid, kThreads, 0, s>>>(a);
-    else crc32c_span_kernel<true, false><<<grid, kThreads, 0, s>>>(a);
-  } else {
-    if (a.pair_kernel && !skip) crc32c_pair_kernel<false><<<grid, kThreads, 0, s>>>(a);
-    if (skip) crc32c_span_kernel<false, true><<<grid, kThreads, 0, s>>>(a);
-    else crc32c_span_kernel<false, false><<<grid, kThreads, 0, s>>>(a);
+    if (skip) return launch_k(crc32c_span_kernel<true, true>, dim3(grid), dim3(kThreads), s, stop, a);
+    return launch_k(crc32c_span_kernel<true, false>, dim3(grid), dim3(kThreads), s, stop, a);
   }
-  return hipGetLastError();
+  if (a.pair_kernel && !skip) crc32c_pair_kernel<false><<<grid, kThreads, 0, s>>>(a);
+  if (skip) return launch_k(crc32c_span_kernel<false, true>, dim3(grid), dim3(kThreads), s, stop, a);
+  return launch_k(crc32c_span_kernel<false, false>, dim3(grid), dim3(kThreads), s, stop, a);
 }
 
 hipError_t launch_fixed(const SpanBatch& a, bool verify, int grid, hipStream_t s) {
@@ -1648,16 +1663,14 @@ hipError_t launch_fixed(const SpanBatch& a, bool verify, int grid, hipStream_t s
   return hipGetLastError();
 }
 
-hipError_t launch_plan(const SpanBatch& a, bool desc, const SplitWs& ws, hipStream_t s) {
-  if (desc) crc32c_plan_kernel<true><<<ws.nblocks, kPlanThreads, 0, s>>>(a, ws);
-  else crc32c_plan_kernel<false><<<ws.nblocks, kPlanThreads, 0, s>>>(a, ws);
-  return hipGetLastError();
+hipError_t launch_plan(const SpanBatch& a, bool desc, const SplitWs& ws, hipStream_t s, hipEvent_t stop) {
+  if (desc) return launch_k(crc32c_plan_kernel<true>, dim3(ws.nblocks), dim3(kPlanThreads), s, stop, a, ws);
+  return launch_k(crc32c_plan_kernel<false>, dim3(ws.nblocks), dim3(kPlanThreads), s, stop, a, ws);
 }
 
-hipError_t launch_slices(const SpanBatch& a, const SplitWs& ws, hipStream_t s) {
+hipError_t launch_slices(const SpanBatch& a, const SplitWs& ws, hipStream_t s, hipEvent_t stop) {
   crc32c_slice_scan_kernel<<<1, 1024, 0, s>>>(a, ws);
-  crc32c_slice_mark_kernel<<<ws.nblocks, kPlanThreads, 0, s>>>(a, ws);
-  return hipGetLastError();
+  return launch_k(crc32c_slice_mark_kernel, dim3(ws.nblocks), dim3(kPlanThreads), s, stop, a, ws);
 }
 
 hipError_t launch_long_list(const SpanBatch& a, const SplitWs& ws, hipStream_t s) {
@@ -1677,30 +1690,26 @@ hipError_t launch_lane(const SpanBatch& a, bool verify, int grid, hipStream_t s)
 }
 
 hipError_t launch_scatter(const SpanBatch& a, const SplitWs& ws, const uint32_t* qout, const uint8_t* qmm,
-                          hipStream_t s) {
-  crc32c_scatter_kernel<<<256, 256, 0, s>>>(a, ws, qout, qmm);
-  return hipGetLastError();
+                          hipStream_t s, hipEvent_t stop) {
+  return launch_k(crc32c_scatter_kernel, dim3(256), dim3(256), s, stop, a, ws, qout, qmm);
 }
 
-hipError_t launch_trailers(const SpanBatch& a, bool desc, const uint32_t* res, hipStream_t s) {
+hipError_t launch_trailers(const SpanBatch& a, bool desc, const uint32_t* res, hipStream_t s, hipEvent_t stop) {
   const uint64_t blocks = (a.n + 255u) / 256u;
   const int grid = (int)(blocks < 16384u ? blocks : 16384u);
-  if (desc) crc32c_trailer_kernel<true><<<grid, 256, 0, s>>>(a, res);
-  else crc32c_trailer_kernel<false><<<grid, 256, 0, s>>>(a, res);
-  return hipGetLastError();
+  if (desc) return launch_k(crc32c_trailer_kernel<true>, dim3(grid), dim3(256), s, stop, a, res);
+  return launch_k(crc32c_trailer_kernel<false>, dim3(grid), dim3(256), s, stop, a, res);
 }
 
-hipError_t launch_combine(const SpanBatch& a, bool desc, bool verify, const SplitWs& ws,
-                          hipStream_t s) {
-  const int grid = 256;  // 1024 waves, one long span each at a time
+hipError_t launch_combine(const SpanBatch& a, bool desc, bool verify, const SplitWs& ws, hipStream_t s,
+                          hipEvent_t stop) {
+  const dim3 grid(256), block(256);  // 1024 waves, one long span each at a time
   if (desc) {
-    if (verify) crc32c_combine_kernel<true, true><<<grid, 256, 0, s>>>(a, ws);
-    else crc32c_combine_kernel<true, false><<<grid, 256, 0, s>>>(a, ws);
-  } else {
-    if (verify) crc32c_combine_kernel<false, true><<<grid, 256, 0, s>>>(a, ws);
-    else crc32c_combine_kernel<false, false><<<grid, 256, 0, s>>>(a, ws);
+    if (verify) return launch_k(crc32c_combine_kernel<true, true>, grid, block, s, stop, a, ws);
+    return launch_k(crc32c_combine_kernel<true, false>, grid, block, s, stop, a, ws);
   }
-  return hipGetLastError();
+  if (verify) return launch_k(crc32c_combine_kernel<false, true>, grid, block, s, stop, a, ws);
+  return launch_k(crc32c_combine_kernel<false, false>, grid, block, s, stop, a, ws);
 }
 
 }  // namespace dev
