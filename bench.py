@@ -56,9 +56,9 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
-# config5_leg times windows next to the planner path with the library's
-# prismdb_crc32c_windows setter, which acts only with this set
-os.environ.setdefault("PRISMDB_ENABLE_TEST_HOOKS", "1")
+# (The measured process runs with the library's test hooks off: every leg
+# takes the default routes a PrismDB caller gets.  tools/bench_configs.py
+# times pinned routes side by side.)
 
 METRIC = "GiB/s CRC32C over device-resident 4 KiB SST blocks; bit-exact vs util/crc32c.cc"
 SEED = 0x5EED0001
@@ -527,15 +527,6 @@ def config5_leg(args, torch, dist, crc32c, dev, rank, world) -> dict:
     seal = leg(False, 1)
     verify = leg(True, 1)
     comp = {str(k): {"seal": leg(False, k), "verify": leg(True, k)} for k in kpcs}
-    from prismdb_amd._lib import lib as _native
-    for k in kpcs:
-        if k * spf > (1 << 17):  # more than one launch takes: the planner path (default) next to windows
-            prev = _native().prismdb_crc32c_windows(1)
-            try:
-                comp[str(k)]["seal_windows"] = leg(False, k)
-                comp[str(k)]["verify_windows"] = leg(True, k)
-            finally:
-                _native().prismdb_crc32c_windows(prev)
     torch.cuda.synchronize()
     bad = int(mm.sum().item())
     unmasked = (out.to(torch.int64) & 0xFFFFFFFF) - 0xA282EAD8

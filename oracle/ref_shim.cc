@@ -1,4 +1,6 @@
-// ref_shim.cc -- TEST INFRASTRUCTURE ONLY (oracle/_ref build, never shipped).
+// ref_shim.cc -- TEST INFRASTRUCTURE ONLY (oracle/_ref build: not part of the
+// product library; the built .so travels to the GPU box with the tree, where
+// bench.py's cpu_baseline loads it as the reference CPU path).
 //
 // A thin extern "C" face over the reference's own crc32c::Extend, compiled
 // together with /root/reference/util/crc32c.cc by oracle/Makefile into

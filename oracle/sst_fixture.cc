@@ -1,4 +1,6 @@
-// sst_fixture.cc -- TEST INFRASTRUCTURE ONLY (fixture generator, never shipped).
+// sst_fixture.cc -- TEST INFRASTRUCTURE ONLY (fixture generator: not part of
+// the product library; the built binary travels to the GPU box with the tree,
+// where tests/test_gpu_sst_full.py runs it to write a full-size reference table).
 //
 // Drives the reference TableBuilder (table/table_builder.cc, compiled from
 // /root/reference by oracle/Makefile) to write a small SST shaped like

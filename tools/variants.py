@@ -520,8 +520,11 @@ VARIANTS["direct_ts_plain"] = VARIANTS["direct_ts"] + VARIANTS["direct_plain"]
 # the trailer pass's stores plain (write-back through L2) instead of
 # non-temporal: 2.4 M scattered dword stores took the pass 117 us on a config-5
 # call, the same stores from a bare kernel 38 us (tools/trailer_probe.py)
-VARIANTS["trail_plain"] = [("crc32c_kernels.hip", TRAIL_STORE,
-                            '    asm volatile("global_store_dword %0, %1, off" : : "v"(t), "v"(res[i]) : "memory");\n  }\n}\n')]
+# (since adopted; then one span per thread, "trail_x1", against four)
+VARIANTS["trail_x1"] = [("crc32c_kernels.hip", "constexpr uint32_t kTrailPer = 4;", "constexpr uint32_t kTrailPer = 1;")]
+VARIANTS["trail_nt"] = [("crc32c_kernels.hip",
+                         '      if (t[k] != nullptr) asm volatile("global_store_dword %0, %1, off" : : "v"(t[k]), "v"(v[k]) : "memory");\n',
+                         '      if (t[k] != nullptr) store_le32(t[k], v[k]);\n')]
 
 
 def do_build(names):
