@@ -73,14 +73,15 @@ def parse(path):
             e -= 1
         calls.append(rows[b:e])
     seal = [c for c in calls if any("crc32c_trailer_kernel" in r["Kernel_Name"] for r in c)]
-    ver = [c for c in calls if c not in seal and any("pair_kernel<true>" in r["Kernel_Name"] for r in c)]
+    ver = [c for c in calls if c not in seal and any(k in r["Kernel_Name"] for r in c
+                                                      for k in ("pair_kernel<true>", "bulk_kernel<true>"))]
     for name, group in (("seal", seal), ("verify", ver)):
         if not group:
             continue
         c = [r for r in group[-1] if "crc32c" in r["Kernel_Name"]]
         t0 = int(c[0]["Start_Timestamp"])
         t1 = max(int(r["End_Timestamp"]) for r in c)
-        pair = [r for r in c if "crc32c_pair_kernel" in r["Kernel_Name"]]
+        pair = [r for r in c if "crc32c_pair_kernel" in r["Kernel_Name"] or "crc32c_bulk_kernel" in r["Kernel_Name"]]
         print(f"# {name}: call {(t1 - t0) / 1e3:.1f} us")
         print("start_us,duration_us,queue,kernel")
         for r in c:
