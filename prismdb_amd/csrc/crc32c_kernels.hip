@@ -1600,39 +1600,22 @@ __global__ __launch_bounds__(256) void crc32c_scatter_kernel(SpanBatch a, SplitW
 // whatever their cache policy: profiles/r05/r05b_variants_pair_seal.json);
 // the one-launch kernel, whose trailers go out together at the end of each
 // wave's run, seals almost free.  So the trailers of a bulk batch go out
-// here, in one burst after the reads: kTrailPer spans per thread (their
-// descriptor and result loads all issued before the first store), read
-// coalesced.  The stores are plain (write-back through L2), not the
-// non-temporal stores of the kernels that seal as they read: on a config-5
-// call (2.4 M trailers) the non-temporal pass took 117 us, a bare kernel
-// storing the same dwords plainly 38 us (tools/trailer_probe.py,
-// profiles/r06/r06i_trailer_probe.json), and the config-5 seal call went from
-// 1.929 to 1.893 ms with only this pass's stores made plain
-// (profiles/r06/r06j_variants_trail.json).
+// here, in one burst after the reads: one thread per span, descriptors and
+// results read coalesced, non-temporal stores.  (Plain stores, four spans per
+// thread, took this pass from 117 to 77 us on a config-5 call but left 2.4 M
+// dirty partial lines behind, whose write-back then ran under the next call:
+// six config-5 seals back to back took 2.022 ms each against 1.682 ms,
+// profiles/r06/r06n_variants.json, r06l config5_one_process.)
 // ---------------------------------------------------------------------------
-constexpr uint32_t kTrailPer = 4;
 template <bool kDesc>
 __global__ __launch_bounds__(256) void crc32c_trailer_kernel(SpanBatch a, const uint32_t* res) {
   const bool hdr = (a.flags & kFlagLogHeader) != 0;
   const uint64_t step = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i0 < a.n; i0 += step * kTrailPer) {
-    const uint8_t* t[kTrailPer];
-    uint32_t v[kTrailPer];
-#pragma unroll
-    for (uint32_t k = 0; k < kTrailPer; ++k) {
-      const uint64_t i = i0 + k * step;
-      t[k] = nullptr;
-      v[k] = 0;
-      if (i < a.n) {
-        const uint64_t off = kDesc ? a.off[i] : i * a.stride;
-        const uint32_t len = kDesc ? a.len[i] : a.len_c;
-        t[k] = hdr ? a.base + off - kLogCrcBack : a.base + off + len;
-        v[k] = res[i];
-      }
-    }
-#pragma unroll
-    for (uint32_t k = 0; k < kTrailPer; ++k)
-      if (t[k] != nullptr) asm volatile("global_store_dword %0, %1, off" : : "v"(t[k]), "v"(v[k]) : "memory");
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += step) {
+    const uint64_t off = kDesc ? a.off[i] : i * a.stride;
+    const uint32_t len = kDesc ? a.len[i] : a.len_c;
+    const uint8_t* t = hdr ? a.base + off - kLogCrcBack : a.base + off + len;
+    store_le32(t, res[i]);
   }
 }
 
@@ -1716,7 +1699,7 @@ hipError_t launch_scatter(const SpanBatch& a, const SplitWs& ws, const uint32_t*
 }
 
 hipError_t launch_trailers(const SpanBatch& a, bool desc, const uint32_t* res, hipStream_t s, hipEvent_t stop) {
-  const uint64_t blocks = (a.n + 256u * kTrailPer - 1u) / (256u * kTrailPer);
+  const uint64_t blocks = (a.n + 255u) / 256u;
   const int grid = (int)(blocks < 16384u ? blocks : 16384u);
   if (desc) return launch_k(crc32c_trailer_kernel<true>, dim3(grid), dim3(256), s, stop, a, res);
   return launch_k(crc32c_trailer_kernel<false>, dim3(grid), dim3(256), s, stop, a, res);

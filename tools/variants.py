@@ -271,6 +271,10 @@ VARIANTS = {
 # the previous commit's kernels (a git worktree under build/:
 # `git worktree add --detach build/wt_head HEAD`)
 VARIANTS["prev"] = [("@src", os.path.join(ROOT, "build", "wt_head", "prismdb_amd", "csrc"), None)]
+# other checkouts (git worktree add build/wt_<rev> <rev>): round 5's product,
+# and round 6's planner lead-in change alone
+VARIANTS["r05"] = [("@src", os.path.join(ROOT, "build", "wt_0f74c91", "prismdb_amd", "csrc"), None)]
+VARIANTS["r06_parity"] = [("@src", os.path.join(ROOT, "build", "wt_72d150e", "prismdb_amd", "csrc"), None)]
 # walsafe: walsec + the neighbour check (flag bit 26 of the lane's meta)
 VARIANTS["walsafe"] = [
     (f, o, n.replace("const uint64_t sa = owned && lastk ?", "const uint64_t sa = owned && lastk && ((vmeta >> 26) & 1u) ?")
@@ -520,11 +524,15 @@ VARIANTS["direct_ts_plain"] = VARIANTS["direct_ts"] + VARIANTS["direct_plain"]
 # the trailer pass's stores plain (write-back through L2) instead of
 # non-temporal: 2.4 M scattered dword stores took the pass 117 us on a config-5
 # call, the same stores from a bare kernel 38 us (tools/trailer_probe.py)
-# (since adopted; then one span per thread, "trail_x1", against four)
-VARIANTS["trail_x1"] = [("crc32c_kernels.hip", "constexpr uint32_t kTrailPer = 4;", "constexpr uint32_t kTrailPer = 1;")]
-VARIANTS["trail_nt"] = [("crc32c_kernels.hip",
-                         '      if (t[k] != nullptr) asm volatile("global_store_dword %0, %1, off" : : "v"(t[k]), "v"(v[k]) : "memory");\n',
-                         '      if (t[k] != nullptr) store_le32(t[k], v[k]);\n')]
+# log-record seals through the trailer pass too (the lane kernel then stores
+# no header crcs; round 5 measured the pass 5 % behind the lane kernel's own
+# stores, r05g_variants_lane_seal)
+VARIANTS["lane_pass"] = [("crc32c_capi.hip",
+                          "  const bool trailer_pass = (a.flags & prismdb::dev::kFlagWriteTrailer) != 0 && !lane;\n",
+                          "  const bool trailer_pass = (a.flags & prismdb::dev::kFlagWriteTrailer) != 0;\n")]
+# (trail_plain was adopted in 15de4d0 -- plain stores, four spans per thread,
+# variants trail_x1 / trail_nt there -- and reverted: its dirty lines cost the
+# next call more than the pass saved, profiles/r06/r06n_variants.json)
 
 
 def do_build(names):
@@ -643,7 +651,7 @@ def do_run(args, names):
     f2n, f3n = 2 * (nfd + 1), 3 * (nfd + 1)  # two and three files: either side of the two-sequence limit
     f7out = torch.empty(7 * (nfd + 1), dtype=torch.int32, device=dev)
     f7mm = torch.empty(7 * (nfd + 1), dtype=torch.uint8, device=dev)
-    calls = {"file_fixed": 50, "file_desc": 50, "file_seal": 50, "file_verify": 50, "tiny_desc": 50,
+    calls = {"sst_c5_seal": 6, "file_fixed": 50, "file_desc": 50, "file_seal": 50, "file_verify": 50, "tiny_desc": 50,
              "files7_seal": 10, "files7_verify": 10, "files2_seal": 20, "files2_verify": 20,
              "files3_seal": 20, "files3_verify": 20}
     work = {
