@@ -432,6 +432,11 @@ VARIANTS["lane_head"] = [("crc32c_kernels.hip", "@git", "HEAD:prismdb_amd/csrc/c
 # written as the whole aligned 32-B sector(s) around it, read first, instead
 # of one 4-B partial write: do full-sector writes beat the partial ones?
 TRAIL_STORE = "    store_le32(t, res[i]);\n  }\n}\n"
+TRAIL_LOOP = ("  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += step) {\n"
+              "    const uint64_t off = kDesc ? a.off[i] : i * a.stride;\n"
+              "    const uint32_t len = kDesc ? a.len[i] : a.len_c;\n"
+              "    const uint8_t* t = hdr ? a.base + off - kLogCrcBack : a.base + off + len;\n"
+              "    store_le32(t, res[i]);\n  }\n}\n")
 VARIANTS["trail_sector"] = [("crc32c_kernels.hip", TRAIL_STORE,
     "    {\n"
     "      const uint64_t ta = reinterpret_cast<uint64_t>(t), s0 = ta & ~31ull, s1 = (ta + 3u) & ~31ull;\n"
@@ -530,6 +535,19 @@ VARIANTS["direct_ts_plain"] = VARIANTS["direct_ts"] + VARIANTS["direct_plain"]
 VARIANTS["lane_pass"] = [("crc32c_capi.hip",
                           "  const bool trailer_pass = (a.flags & prismdb::dev::kFlagWriteTrailer) != 0 && !lane;\n",
                           "  const bool trailer_pass = (a.flags & prismdb::dev::kFlagWriteTrailer) != 0;\n")]
+# the non-temporal trailer pass with four spans per thread, loads first
+VARIANTS["trail_nt4"] = [("crc32c_kernels.hip", TRAIL_LOOP,
+    "  for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i0 < a.n; i0 += step * 4u) {\n"
+    "    const uint8_t* t[4];\n    uint32_t v[4];\n"
+    "#pragma unroll\n    for (uint32_t k = 0; k < 4u; ++k) {\n"
+    "      const uint64_t i = i0 + k * step;\n      t[k] = nullptr;\n      v[k] = 0u;\n"
+    "      if (i < a.n) {\n"
+    "        const uint64_t off = kDesc ? a.off[i] : i * a.stride;\n"
+    "        const uint32_t len = kDesc ? a.len[i] : a.len_c;\n"
+    "        t[k] = hdr ? a.base + off - kLogCrcBack : a.base + off + len;\n        v[k] = res[i];\n      }\n    }\n"
+    "#pragma unroll\n    for (uint32_t k = 0; k < 4u; ++k)\n      if (t[k] != nullptr) store_le32(t[k], v[k]);\n  }\n}\n"),
+    ("crc32c_kernels.hip", "  const uint64_t blocks = (a.n + 255u) / 256u;\n  const int grid = (int)(blocks < 16384u ? blocks : 16384u);\n  if (desc) return launch_k(crc32c_trailer_kernel",
+     "  const uint64_t blocks = (a.n + 1023u) / 1024u;\n  const int grid = (int)(blocks < 16384u ? blocks : 16384u);\n  if (desc) return launch_k(crc32c_trailer_kernel")]
 # (trail_plain was adopted in 15de4d0 -- plain stores, four spans per thread,
 # variants trail_x1 / trail_nt there -- and reverted: its dirty lines cost the
 # next call more than the pass saved, profiles/r06/r06n_variants.json)
@@ -651,7 +669,7 @@ def do_run(args, names):
     f2n, f3n = 2 * (nfd + 1), 3 * (nfd + 1)  # two and three files: either side of the two-sequence limit
     f7out = torch.empty(7 * (nfd + 1), dtype=torch.int32, device=dev)
     f7mm = torch.empty(7 * (nfd + 1), dtype=torch.uint8, device=dev)
-    calls = {"sst_c5_seal": 6, "file_fixed": 50, "file_desc": 50, "file_seal": 50, "file_verify": 50, "tiny_desc": 50,
+    calls = {"sst_c5_seal": 6, "wal": 3, "wal_seal": 3, "file_fixed": 50, "file_desc": 50, "file_seal": 50, "file_verify": 50, "tiny_desc": 50,
              "files7_seal": 10, "files7_verify": 10, "files2_seal": 20, "files2_verify": 20,
              "files3_seal": 20, "files3_verify": 20}
     work = {
