@@ -100,11 +100,12 @@ int leveldb_crc32c_batch_fixed(const void* dev_base, size_t stride, size_t len, 
  * Variable batch: block i = base[off[i], off[i] + len[i]); init[i] per block
  * (dev_init may be NULL: all 0).  Any byte alignment, any length (< 4 GiB).
  * Long spans are split across many wavefronts and recombined on the device.
- * Routing is by span count alone: <= 2^17 spans one kernel launch (an SST
- * file, a log file); 2^17 < n <= 2^18 spans without LOG_HEADER two such
- * launches (a compaction's dozen files: uniform SST blocks run faster that
- * way, batches of very mixed span sizes ~10 points of roofline slower than on
- * the planner path); beyond, the planner path (task-balanced slices).
+ * Routing: <= 2^17 spans one kernel launch (an SST file, a log file);
+ * 2^17 < n <= 2^18 spans that seal (WRITE_TRAILER) or verify block trailers
+ * (dev_mismatch != NULL), without LOG_HEADER, two such launches (a
+ * compaction's dozen SST files: uniform blocks run faster that way);
+ * everything else the planner path (task-balanced slices: plain checksum
+ * batches of mixed span sizes, log records, any batch beyond 2^18 spans).
  */
 int leveldb_crc32c_batch(const void* dev_base, const uint64_t* dev_off, const uint32_t* dev_len,
                          const uint32_t* dev_init, size_t n, uint32_t* dev_out,

@@ -96,7 +96,8 @@ std::atomic<uint32_t> g_direct_cap{prismdb::dev::kDirectTickets};
 std::atomic<uint32_t> g_direct_dbg{0};
 // Descriptor batches of more than g_direct_max spans (without LOG_HEADER):
 // windows of the one-launch kernel (1), the planner path (0), or (2, the
-// default) windows up to two of them and the planner path beyond.  Two
+// default) windows up to two of them for batches that seal or verify block
+// trailers (RunBatch), the planner path otherwise and beyond.  Two
 // windows of SST files (twelve files, 201 744 spans) take 13.4 us per file,
 // against 21.6 on the planner path, whose 5-7 launches and segment pass cost
 // ~120 us per call; from there on the planner's balance wins, and on mixed
@@ -658,11 +659,19 @@ int RunBatch(DeviceCtx& ctx, const SpanBatch& base_args, bool desc, bool verify,
     hipError_t e = prismdb::dev::launch_direct(a, verify, ctx.cus, d, s, w->done[w->gen & 1u]);
     return e == hipSuccess ? 0 : FailHip(e, "direct kernel launch");
   }
-  // Bulk descriptor batches: windows of the one-launch kernel.
+  // Bulk descriptor batches: windows of the one-launch kernel.  By default
+  // (wmode 2) only batches of <= 2 windows that seal or verify block
+  // trailers: TableBuilder / ReadBlock batches, whose spans are block_size-
+  // bounded data blocks plus one index block per file (uniform: the windows'
+  // static runs balance them).  A plain checksum batch has no such shape and
+  // takes the planner's task-balanced slices: 200 000 config-3 spans (1-64
+  // KiB) ran at 57.5 % of the roofline as windows against 70.5 % on the
+  // planner path (profiles/r06/r06s_configs.json, config3_band).
   const uint64_t wmax = g_direct_max.load(std::memory_order_relaxed);
   const int wmode = g_windows.load(std::memory_order_relaxed);
-  if (desc && route == kRouteAuto && wmax > 0 && a.n > wmax && (wmode == 1 || (wmode == 2 && a.n <= 2 * wmax)) &&
-      !(a.flags & prismdb::dev::kFlagLogHeader))
+  const bool block_trailers = verify || (a.flags & prismdb::dev::kFlagWriteTrailer) != 0;
+  if (desc && route == kRouteAuto && wmax > 0 && a.n > wmax &&
+      (wmode == 1 || (wmode == 2 && a.n <= 2 * wmax && block_trailers)) && !(a.flags & prismdb::dev::kFlagLogHeader))
     return RunWindows(ctx, base_args, verify, s, wmax);
   // The span kernel indexes records with 32 bits: cut larger batches.
   if (a.n > prismdb::dev::kMaxGenericSpans) {

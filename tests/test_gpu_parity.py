@@ -1248,3 +1248,35 @@ def test_lane_runs_without_owned_records(dev, oracle, native, layout):
         restore()
     for o in outs:
         np.testing.assert_array_equal(_u32(o), want)
+
+
+def test_band_routing_by_caller_intent(dev, oracle, native):
+    """2^17 < n <= 2^18 spans with the default routing: a plain checksum batch
+    takes the planner path, the same spans sealed or verified take two
+    windows of the one-launch kernel (include/prismdb_crc32c.h); bit-exact on
+    every route."""
+    import torch
+    from prismdb_amd import crc32c
+
+    rng = np.random.default_rng(0x5EED0090)
+    n = 150_000
+    lens = rng.choice([100, 1000, 3000, 9000], size=n).astype(np.uint64)
+    off = np.cumsum(np.concatenate([[8], (lens + 4)[:-1]])).astype(np.uint64)
+    host = oracle.synth(int(off[-1] + lens[-1]) + 64, 0x5EED0091)
+    raw, _ = oracle.batch(host, off, lens)
+    buf = torch.from_numpy(host).to(dev)
+    d_off = torch.from_numpy(off.astype(np.int64)).to(dev)
+    d_len = torch.from_numpy(lens.astype(np.uint32).view(np.int32)).to(dev)
+    assert native.prismdb_crc32c_windows(2) == 2 and native.prismdb_crc32c_direct_max(1 << 17) == 1 << 17
+    sched = (ctypes.c_uint64 * 3)()
+    out, _ = crc32c.batch(buf, d_off, d_len)
+    assert native.prismdb_crc32c_last_schedule(sched) == 0  # the planner path
+    np.testing.assert_array_equal(_u32(out), raw)
+    out, _ = crc32c.batch(buf, d_off, d_len, mask=True, trailer=True)
+    assert native.prismdb_crc32c_last_schedule(sched) == -2  # windows of the one-launch kernel
+    masked = np.array([oracle.mask(int(c)) for c in raw], dtype=np.uint32)
+    np.testing.assert_array_equal(_u32(out), masked)
+    out, mm = crc32c.batch(buf, d_off, d_len, verify=True)
+    assert native.prismdb_crc32c_last_schedule(sched) == -2
+    np.testing.assert_array_equal(_u32(out), raw)
+    assert not mm.cpu().numpy().any()

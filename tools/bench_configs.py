@@ -9,7 +9,9 @@ of the algorithmic bytes (fixed L+4; variable L+4+12; verify
 L+4+1 per span):
   config3_mixed      spans of 1/4/16/64 KiB (uniform, seed 0x5EED0003) packed back to back, ~16 GiB
   *_windows          the same batch as windows of 2^17 spans of the one-launch kernel, back to back
-                     (the default for > 2^17 spans is the planner path)
+                     (the default for > 2^18 spans is the planner path)
+  config3_band       200 000 of those spans: the 2^17..2^18 band whose default is two windows;
+                     *_planner the planner path pinned
   sst_fixed          3988-B spans (YCSB data block + type byte) at stride 3992, 16 Mi spans (~62.4 GiB)
   sst_desc           same spans through descriptors + one 486 977-B index span per 16 811 (split path)
   verify_4k          ReadBlock-verify of 16 Mi x (4092 + type... ) 4 KiB spans with stored trailers
@@ -96,6 +98,29 @@ def main():
         report("config3_mixed_windows", timed(windows(fn), args.reps), lens.sum(), lens.sum() + 16 * len(lens),
                len(lens))
         res["config3_mixed_windows"]["agrees"] = bool(torch.equal(ref, out))
+        del d_off, d_len, out
+    if want("config3_band"):
+        # 200 000 config-3 spans: inside 2^17 < n <= 2^18, where the default
+        # route is two windows of the one-launch kernel; the planner path (and
+        # the windows pinned) next to it
+        m = 200_000
+        bl = lens[:m]
+        off = np.concatenate([[0], np.cumsum(bl)[:-1]])
+        d_off, d_len = torch.from_numpy(off).to(dev), torch.from_numpy(bl.astype(np.int32)).to(dev)
+        out = torch.empty(m, dtype=torch.int32, device=dev)
+        fn = lambda: crc32c.batch(buf, d_off, d_len, out=out, check_bounds=False)  # noqa: E731
+        report("config3_band", timed(fn, args.reps), bl.sum(), bl.sum() + 16 * m, m)
+        ref = out.clone()
+
+        def planner():
+            prev = native().prismdb_crc32c_windows(0)
+            try:
+                fn()
+            finally:
+                native().prismdb_crc32c_windows(prev)
+        report("config3_band_planner", timed(planner, args.reps), bl.sum(), bl.sum() + 16 * m, m)
+        res["config3_band_planner"]["agrees"] = bool(torch.equal(ref, out))
+        report("config3_band_windows", timed(windows(fn), args.reps), bl.sum(), bl.sum() + 16 * m, m)
         del d_off, d_len, out
     if want("config3_seal"):
         # the same span sizes sealed (MASK | WRITE_TRAILER): a 4-B trailer slot after each span
