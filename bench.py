@@ -630,6 +630,13 @@ def multi_leg(args, torch, crc32c, ndev: int) -> dict:
                 res[name]["per_device_gather_ms"] = tm["gather_ms"]
                 res[name]["per_device_GiB_s"] = [round(nfiles * span_bytes / (b / 1e3) / GIB, 1) if b > 0 else None
                                                  for b in tm["batch_ms"]]
+            # the same call's host side: when each partition's enqueue started
+            # (partitions > 0 on their devices' worker threads) and how long it took
+            ht = crc32c.multi_host_timing(list(range(ndev)))
+            if ht is not None:
+                res[name]["host_enqueue_start_us"] = ht["start_us"]
+                res[name]["host_enqueue_us"] = ht["enqueue_us"]
+                res[name]["host_call_us"] = ht["call_us"]
     want = torch.cat([t.to(root) for t in sep])
     res["gather_check"] = {"gathered_equals_per_device": bool(torch.equal(out, want)), "entries": int(out.numel())}
     crc32c.batch_multi(parts, verify=True, out=out, mismatch=mm, streams=streams, check_bounds=False)
