@@ -37,7 +37,8 @@ Printed (rank 0): ONE JSON line with the driver's contract fields plus
                 util/env_posix.cc:850-890); one RCCL clique of N devices
                 (ncclCommInitAll), results gathered to device 0 over xGMI;
                 per device its batch and gather times (HIP events on the
-                clique streams) and the clique's ncclCommInitAll wall time
+                clique streams), each partition's host enqueue start and
+                duration, and the clique's ncclCommInitAll wall time
                 (--no-multi skips it; at N = 1, --multi-devices picks the
                 device count, default 1)
 """
@@ -81,7 +82,9 @@ def parse():
     ap.add_argument("--e2e", action="store_true", help="also measure the host-resident (pinned copy) rate")
     ap.add_argument("--no-config5", action="store_true", help="skip the config-5 partition leg")
     ap.add_argument("--c5-spans", type=int, default=2_400_000, help="config-5 spans per partition (GPU)")
-    ap.add_argument("--c5-steps", type=int, default=5)
+    # (20, as the headline's steps: at 5 the first call's launch latency and
+    # the closing synchronisation were ~1.5 % of a one-process config-5 round)
+    ap.add_argument("--c5-steps", type=int, default=20)
     ap.add_argument("--c5-files-per-call", default="7,12",
                     help="config-5 compaction legs: SST files per leveldb_crc32c_batch call (comma list; 7 files "
                          "are the most one launch takes, 12 a compaction's input set: 1 file + ~11 overlapping)")
