@@ -622,7 +622,11 @@ def multi_leg(args, torch, crc32c, ndev: int) -> dict:
         res[name] = {"value": round(ndev * nfiles * span_bytes * args.c5_steps / el / GIB, 2), "unit": "GiB/s",
                      "ms_per_step": round(el * 1e3 / args.c5_steps, 3), "rounds": 3, "stat": "median round"}
         if name == "with_gather":
-            fn()  # the timing diagnostics below read this call's phases
+            # the timing diagnostics below read the second call's phases: it is
+            # enqueued while the first runs, as in the timed steps (a call made
+            # right after a synchronisation took ~3x the host time)
+            fn()
+            fn()
             sync_all()
             # the last step's phases on each device (HIP events on the clique
             # streams) and the clique's one-time ncclCommInitAll
