@@ -548,6 +548,29 @@ VARIANTS["trail_nt4"] = [("crc32c_kernels.hip", TRAIL_LOOP,
     "#pragma unroll\n    for (uint32_t k = 0; k < 4u; ++k)\n      if (t[k] != nullptr) store_le32(t[k], v[k]);\n  }\n}\n"),
     ("crc32c_kernels.hip", "  const uint64_t blocks = (a.n + 255u) / 256u;\n  const int grid = (int)(blocks < 16384u ? blocks : 16384u);\n  if (desc) return launch_k(crc32c_trailer_kernel",
      "  const uint64_t blocks = (a.n + 1023u) / 1024u;\n  const int grid = (int)(blocks < 16384u ? blocks : 16384u);\n  if (desc) return launch_k(crc32c_trailer_kernel")]
+# the sealing lane kernel's header store held back to the next slot's wait
+# and issued right after it, before that slot's fold: the store's write
+# acknowledgement sits in the in-order vmcnt, and issued at the end of the
+# fold it was waited for by the very next counted wait (profiles/r06/r06p_wal_pmc:
+# TCP pending stalls 2x verify's); here the fold's work overlaps it
+VARIANTS["lane_st_late"] = [
+    ("crc32c_kernels.hip", "  u32x4 W[2][8];\n",
+     "  u32x4 W[2][8];\n  uint64_t st_ta = 0;\n  uint32_t st_v = 0u, st_pend = 0u;  // a header store held back (seal)\n"),
+    ("crc32c_kernels.hip",
+     "          const uint64_t ta = hdr ? VP[sl] - kLogCrcBack : VP[sl] + len;\n"
+     '          asm volatile("global_store_dword %0, %1, off" : : "v"(ta), "v"(v) : "memory");\n',
+     "          st_ta = hdr ? VP[sl] - kLogCrcBack : VP[sl] + len;\n          st_v = v;\n          st_pend = 1u;\n"),
+    ("crc32c_kernels.hip",
+     "      wait_lane(W[sl], HD[sl], ED[sl], SC[sl], noff, nlen, ninit);\n",
+     "      wait_lane(W[sl], HD[sl], ED[sl], SC[sl], noff, nlen, ninit);\n"
+     "      if (!kVerify && st_pend != 0u) {\n"
+     '        asm volatile("global_store_dword %0, %1, off" : : "v"(st_ta), "v"(st_v) : "memory");\n'
+     "        st_pend = 0u;\n      }\n"),
+    ("crc32c_kernels.hip",
+     'drained:\n  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");\n',
+     'drained:\n  if (!kVerify && st_pend != 0u) asm volatile("global_store_dword %0, %1, off" : : "v"(st_ta), "v"(st_v) : "memory");\n'
+     '  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");\n'),
+]
 # (trail_plain was adopted in 15de4d0 -- plain stores, four spans per thread,
 # variants trail_x1 / trail_nt there -- and reverted: its dirty lines cost the
 # next call more than the pass saved, profiles/r06/r06n_variants.json)
