@@ -8,6 +8,8 @@
 //                   launch or hipExtLaunchKernel with a stop event (as the
 //                   one-launch kernel is launched)
 //   probe_waves     the same grid, each wave storing its entry and exit
+//   probe_record    hipEventRecord of an event made with given flags (a marker
+//                   packet; system- or agent-scope release)
 //   probe_scatter   one 4-byte store per thread at a stride (dirty lines left
 //                   in L2 at the kernel's end, as the trailer stores leave them)
 // Build: hipcc --offload-arch=gfx950 -O3 -fPIC -shared (tools/percall_floor.py build).
@@ -132,5 +134,16 @@ int probe_read(const void* p, uint64_t bytes, int grid, void* out, void* s) {
 }
 
 int probe_event_create(void** ev) { return (int)hipEventCreateWithFlags(reinterpret_cast<hipEvent_t*>(ev), 0); }
+
+// an event with explicit flags: hipEventDisableTiming (2) as the product's
+// done events, | hipEventDisableSystemFence (0x20000000): its record releases
+// at agent scope instead of system scope
+int probe_event_create_flags(void** ev, unsigned flags) {
+  return (int)hipEventCreateWithFlags(reinterpret_cast<hipEvent_t*>(ev), flags);
+}
+
+int probe_record(void* ev, void* s) {
+  return (int)hipEventRecord(static_cast<hipEvent_t>(ev), static_cast<hipStream_t>(s));
+}
 
 }  // extern "C"

@@ -16,6 +16,13 @@ bracket in us, minus nothing: rows are read against each other.
   empty_call            a 1-span leveldb_crc32c_batch    (one-launch path)
   file_seal / _verify   one SST file (16 811 x 3988 B @ 3992 + 486 977 B index), one call
   fixed_same_bytes      leveldb_crc32c_batch_fixed over 16 480 x 4096 B (the file's 67.5 MB)
+  null_ext_<flags> / null_rec_<flags> / scatter_rec_<flags>_x10
+                        the empty kernel with a stop event / a recorded event, and
+                        16 811 scattered stores + a recorded event, for events made
+                        with hipEventDisableTiming (the product's), | DisableSystemFence,
+                        | ReleaseToDevice, or no flags
+  <variant>_file_*      the file rows through variants base / ev_nofence / ev_device
+                        (the library's own events with those flags)
   file_verify_x10       ten file calls back to back in one bracket (/10: what bench's
                         config5_partitions per-file figure sees)
 and, with the direct_ts variants (per-wave stamps), the one-file call's
@@ -35,6 +42,8 @@ PROBE_DIR = os.path.join(ROOT, "tools", "probe_lib")
 PROBE = os.path.join(PROBE_DIR, "libfloor_probe.so")
 VLIB = os.path.join(ROOT, "tools", "vlib")
 ND, DATA, STRIDE, INDEX = 16811, 3988, 3992, 486977
+EVENT_VARIANTS = ("base", "ev_nofence", "ev_device")
+EVENT_FLAGS = {"default": 0, "notiming": 2, "nofence": 2 | 0x20000000, "todevice": 2 | 0x40000000}
 
 
 def build():
@@ -42,7 +51,7 @@ def build():
     subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-fPIC", "-shared",
                            os.path.join(ROOT, "tools", "floor_probe.hip"), "-o", PROBE])
     subprocess.check_call([sys.executable, os.path.join(ROOT, "tools", "variants.py"), "build", "--only",
-                           "direct_ts", "direct_plain", "direct_ts_plain"])
+                           "direct_ts", "direct_plain", "direct_ts_plain", *EVENT_VARIANTS])
 
 
 def _lib(path):
@@ -71,6 +80,8 @@ def run(reps):
     P.probe_waves.argtypes = [ctypes.c_int, ctypes.c_int, vp, vp]
     P.probe_scatter.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, vp]
     P.probe_event_create.argtypes = [vp]
+    P.probe_event_create_flags.argtypes = [vp, ctypes.c_uint]
+    P.probe_record.argtypes = [vp, vp]
     P.probe_lds.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, vp]
     P.probe_read.argtypes = [vp, ctypes.c_uint64, ctypes.c_int, vp, vp]
     ev = ctypes.c_void_p()
@@ -126,8 +137,18 @@ def run(reps):
     rows["stamp_only"] = bracket(lambda: None)
     rows["null_plain"] = bracket(lambda: P.probe_null(cus, 768, sp, None))
     rows["null_ext"] = bracket(lambda: P.probe_null(cus, 768, sp, ev))
-    rows["waves"] = bracket(lambda: P.probe_waves(cus, 768, ctypes.c_void_p(wave_ts.data_ptr()), sp))
+    # the same with events of explicit flags: the product's (DisableTiming), and
+    # that | DisableSystemFence / | ReleaseToDevice (agent-scope release)
     scat = torch.zeros(ND * STRIDE // 4 + 64, dtype=torch.int32, device=dev)
+    for fname, fl in EVENT_FLAGS.items():
+        e2 = ctypes.c_void_p()
+        assert P.probe_event_create_flags(ctypes.byref(e2), fl) == 0
+        rows[f"null_ext_{fname}"] = bracket(lambda: P.probe_null(cus, 768, sp, e2))
+        rows[f"null_rec_{fname}"] = bracket(lambda: (P.probe_null(cus, 768, sp, None), P.probe_record(e2, sp)))
+        rows[f"scatter_rec_{fname}_x10"] = bracket(
+            lambda: (P.probe_scatter(ctypes.c_void_p(scat.data_ptr()), ND, STRIDE // 4, sp), P.probe_record(e2, sp)),
+            per=10)
+    rows["waves"] = bracket(lambda: P.probe_waves(cus, 768, ctypes.c_void_p(wave_ts.data_ptr()), sp))
     rows["scatter_16811"] = bracket(lambda: P.probe_scatter(ctypes.c_void_p(scat.data_ptr()), ND, STRIDE // 4, sp))
     for lds in (0, 65536, 163840):
         rows[f"lds_{lds}"] = bracket(lambda: P.probe_lds(cus, 768, lds, ctypes.c_void_p(wave_ts.data_ptr()), sp))
@@ -180,6 +201,22 @@ def run(reps):
     rows["hbm_read_67MB_grid4x_x24"] = bracket(
         rot(lambda b: P.probe_read(ctypes.c_void_p(b), ND * STRIDE + INDEX, 4 * cus, ctypes.c_void_p(sink.data_ptr()), sp)),
         per=nf)
+    for name in EVENT_VARIANTS:
+        path = os.path.join(VLIB, f"lib_{name}.so")
+        if not os.path.exists(path):
+            continue
+        V = _lib(path)
+
+        def vfile_at(verify, V=V):
+            def f(base):
+                rc = V.leveldb_crc32c_batch(base, d_off.data_ptr(), d_len.data_ptr(), None, n, out.data_ptr(),
+                                            mm.data_ptr() if verify else None, 0 if verify else 3, sp)
+                assert rc == 0
+            return f
+        rows[f"{name}_file_verify_x10"] = bracket(lambda: call_batch(V, True), per=10)
+        rows[f"{name}_file_seal_x10"] = bracket(lambda: call_batch(V, False), per=10)
+        rows[f"{name}_hbm_file_seal_x24"] = bracket(rot(vfile_at(False)), per=nf)
+        rows[f"{name}_hbm_file_verify_x24"] = bracket(rot(vfile_at(True)), per=nf)
     del big
     res = {"cus": cus, "reps": reps, "file_bytes": int(ND * DATA + INDEX), "rows": rows}
 

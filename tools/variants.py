@@ -571,6 +571,18 @@ VARIANTS["lane_st_late"] = [
      'drained:\n  if (!kVerify && st_pend != 0u) asm volatile("global_store_dword %0, %1, off" : : "v"(st_ta), "v"(st_v) : "memory");\n'
      '  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");\n'),
 ]
+# the library's own events (per-call done events, side-stream fork / join)
+# made with hipEventDisableSystemFence / hipEventReleaseToDevice: their
+# records and stop events release at agent scope, not system scope (no L2
+# write-back at the end of every call)
+def _ev_flags(extra):
+    return [("crc32c_capi.hip", f"hipEventCreateWithFlags(&{v}, hipEventDisableTiming);",
+             f"hipEventCreateWithFlags(&{v}, hipEventDisableTiming | {extra});")
+            for v in ("w.done[0]", "w.done[1]", "w->fork", "w->join")]
+
+
+VARIANTS["ev_nofence"] = _ev_flags("hipEventDisableSystemFence")
+VARIANTS["ev_device"] = _ev_flags("hipEventReleaseToDevice")
 # (trail_plain was adopted in 15de4d0 -- plain stores, four spans per thread,
 # variants trail_x1 / trail_nt there -- and reverted: its dirty lines cost the
 # next call more than the pass saved, profiles/r06/r06n_variants.json)
