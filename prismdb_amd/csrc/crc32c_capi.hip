@@ -819,26 +819,45 @@ int RunBatch(DeviceCtx& ctx, const SpanBatch& base_args, bool desc, bool verify,
   seg.tabs = ctx.tabs;
   seg.rec = ws.seg_rec;
   e = prismdb::dev::launch_span(seg, false, ctx.cus, w->side, w->join);  // the join: its stop event
-  if (e == hipSuccess) e = hipStreamWaitEvent(s, w->join, 0);
   if (e != hipSuccess) return FailHip(e, "segment kernel launch");
-  side_join.armed = false;
   // The call's last kernel completes the workspace's done event itself (its
   // stop event) instead of a marker after it (MarkDone, on an error return).
   hipEvent_t const done = w->done[w->gen & 1u];
-  e = prismdb::dev::launch_combine(a, desc, verify, ws, s, lane || trailer_pass ? nullptr : done);
+  if (trailer_pass) {
+    // Sealing: the trailers of every span but the long ones go out first,
+    // while the segment pass finishes on the side stream; then the join and
+    // the combine, which stores the long spans' trailers with their results.
+    // (Joined first, the pass waited for the segment pass, which ends after
+    // the span kernel, and for the cross-queue wait: a config-5 seal's tail
+    // after the pair-run kernel 144 -> 137.5 us, the join's own ~8 us now
+    // between the pass and the combine; profiles/r06/r06ac_timeline.txt.)
+    SpanBatch t = base_args;
+    t.n = a.n;
+    t.skip_above = prismdb::dev::kLongSpan;
+    t.overflow = &ws.counters->overflow;  // (after an overflow the span pass folded them: no skip)
+    e = prismdb::dev::launch_trailers(t, desc, res_out, s, nullptr);
+    if (e != hipSuccess) return FailHip(e, "trailer kernel launch");
+    e = hipStreamWaitEvent(s, w->join, 0);
+    if (e != hipSuccess) return FailHip(e, "side stream join");
+    side_join.armed = false;
+    SpanBatch c = a;
+    c.flags |= prismdb::dev::kFlagWriteTrailer;
+    e = prismdb::dev::launch_combine(c, desc, verify, ws, s, done);
+    if (e != hipSuccess) return FailHip(e, "combine kernel launch");
+    mark.by_launch = true;
+    return 0;
+  }
+  e = hipStreamWaitEvent(s, w->join, 0);
+  if (e != hipSuccess) return FailHip(e, "side stream join");
+  side_join.armed = false;
+  e = prismdb::dev::launch_combine(a, desc, verify, ws, s, lane ? nullptr : done);
   if (e != hipSuccess) return FailHip(e, "combine kernel launch");
   if (lane) {
     SpanBatch back = a;
     back.out = res_out;
     back.mismatch = caller_mm;
-    e = prismdb::dev::launch_scatter(back, ws, ws.qout, ws.qmm, s, trailer_pass ? nullptr : done);
+    e = prismdb::dev::launch_scatter(back, ws, ws.qout, ws.qmm, s, done);
     if (e != hipSuccess) return FailHip(e, "scatter kernel launch");
-  }
-  if (trailer_pass) {
-    SpanBatch t = base_args;
-    t.n = a.n;
-    e = prismdb::dev::launch_trailers(t, desc, res_out, s, done);
-    if (e != hipSuccess) return FailHip(e, "trailer kernel launch");
   }
   mark.by_launch = true;
   return 0;

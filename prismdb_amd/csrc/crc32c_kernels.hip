@@ -1607,13 +1607,18 @@ __global__ __launch_bounds__(256) void crc32c_scatter_kernel(SpanBatch a, SplitW
 // six config-5 seals back to back took 2.022 ms each against 1.682 ms,
 // profiles/r06/r06n_variants.json, r06l config5_one_process.)
 // ---------------------------------------------------------------------------
+// With a.overflow set, spans longer than a.skip_above are left to the
+// combine kernel (their results are not in yet), unless the segment
+// workspace overflowed and the span pass folded them.
 template <bool kDesc>
 __global__ __launch_bounds__(256) void crc32c_trailer_kernel(SpanBatch a, const uint32_t* res) {
   const bool hdr = (a.flags & kFlagLogHeader) != 0;
+  const uint32_t skip_above = a.overflow != nullptr && *a.overflow == 0u ? a.skip_above : 0xFFFFFFFFu;
   const uint64_t step = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += step) {
     const uint64_t off = kDesc ? a.off[i] : i * a.stride;
     const uint32_t len = kDesc ? a.len[i] : a.len_c;
+    if (len > skip_above) continue;
     const uint8_t* t = hdr ? a.base + off - kLogCrcBack : a.base + off + len;
     store_le32(t, res[i]);
   }

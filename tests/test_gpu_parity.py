@@ -398,6 +398,14 @@ def test_segment_workspace_overflow_fallback(dev, oracle, native, planner_bulk):
     assert (got == wantv).all(), np.flatnonzero(got != wantv)[:10]
     m = mm.cpu().numpy()
     assert np.flatnonzero(m).tolist() == damaged
+    # Sealing the same batch: the overflow again, and the trailer pass then
+    # writes the long spans' trailers too (no combine to leave them to) --
+    # the three damaged trailers are rewritten, the rest rewritten unchanged.
+    out, _ = crc32c.batch(buf, d_off, d_len, d_init, mask=True, trailer=True)
+    assert _last_split(native)[2] == 1
+    assert (_u32(out) == wantv).all()
+    _, mm = crc32c.batch(buf, d_off, d_len, d_init, mask=True, verify=True)
+    assert int(mm.sum().item()) == 0
     del buf, d_off, d_len, d_init, out, mm
     torch.cuda.empty_cache()
 

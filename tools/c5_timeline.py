@@ -2,7 +2,8 @@
 """One config-5 partition call, kernel by kernel (the planner path's lead-in
 and tail around the pair-run kernel).
 
-    python tools/c5_timeline.py run [calls]          # GPU box, under rocprofv3 --kernel-trace
+    python tools/c5_timeline.py run [calls] [variant]  # GPU box, under rocprofv3 --kernel-trace
+                                                     # (variant: tools/vlib/lib_<variant>.so)
     python tools/c5_timeline.py parse <run_kernel_trace.csv>
 
 `run` builds one partition of BASELINE config 5 (143 SST files x (16 811 x
@@ -25,7 +26,9 @@ ND, DATA, STRIDE, INDEX = 16811, 3988, 3992, 486977
 NFILES = 143
 
 
-def run(calls):
+def run(calls, variant=None):
+    import ctypes
+
     import numpy as np
     import torch
 
@@ -47,7 +50,13 @@ def run(calls):
     d_len = torch.from_numpy(lens.astype(np.int32)).to(dev)
     out = torch.empty(n, dtype=torch.int32, device=dev)
     mm = torch.empty(n, dtype=torch.uint8, device=dev)
-    L = lib()
+    if variant:  # a tools/variants.py build instead of the product library
+        L = ctypes.CDLL(os.path.join(ROOT, "tools", "vlib", f"lib_{variant}.so"), mode=os.RTLD_LOCAL)
+        L.leveldb_crc32c_batch.restype = ctypes.c_int
+        L.leveldb_crc32c_batch.argtypes = [ctypes.c_void_p] * 4 + [ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p,
+                                                                   ctypes.c_uint32, ctypes.c_void_p]
+    else:
+        L = lib()
     sp = torch.cuda.current_stream().cuda_stream
     for verify in (False, True):
         for _ in range(calls):
@@ -97,6 +106,6 @@ def parse(path):
 
 if __name__ == "__main__":
     if sys.argv[1] == "run":
-        run(int(sys.argv[2]) if len(sys.argv) > 2 else 5)
+        run(int(sys.argv[2]) if len(sys.argv) > 2 else 5, sys.argv[3] if len(sys.argv) > 3 else None)
     else:
         parse(sys.argv[2])

@@ -529,12 +529,9 @@ VARIANTS["direct_ts_plain"] = VARIANTS["direct_ts"] + VARIANTS["direct_plain"]
 # the trailer pass's stores plain (write-back through L2) instead of
 # non-temporal: 2.4 M scattered dword stores took the pass 117 us on a config-5
 # call, the same stores from a bare kernel 38 us (tools/trailer_probe.py)
-# log-record seals through the trailer pass too (the lane kernel then stores
-# no header crcs; round 5 measured the pass 5 % behind the lane kernel's own
-# stores, r05g_variants_lane_seal)
-VARIANTS["lane_pass"] = [("crc32c_capi.hip",
-                          "  const bool trailer_pass = (a.flags & prismdb::dev::kFlagWriteTrailer) != 0 && !lane;\n",
-                          "  const bool trailer_pass = (a.flags & prismdb::dev::kFlagWriteTrailer) != 0;\n")]
+# (lane_pass -- log-record seals through the trailer pass, -4 %,
+# profiles/r06/r06o -- needs the lane path's scatter before the pass, which
+# the sealing tail no longer runs since the pass moved ahead of the join)
 # the non-temporal trailer pass with four spans per thread, loads first
 VARIANTS["trail_nt4"] = [("crc32c_kernels.hip", TRAIL_LOOP,
     "  for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i0 < a.n; i0 += step * 4u) {\n"
@@ -583,6 +580,37 @@ def _ev_flags(extra):
 
 VARIANTS["ev_nofence"] = _ev_flags("hipEventDisableSystemFence")
 VARIANTS["ev_device"] = _ev_flags("hipEventReleaseToDevice")
+# the plan kernel with its descriptor loads hoisted: each thread loads U
+# spans' (off, len, init) before building any record (the loads of one step
+# in flight together instead of one span's at a time)
+def _plan_hoist(U):
+    src = open(os.path.join(ROOT, "prismdb_amd", "csrc", "crc32c_kernels.hip")).read()
+    a = src.index("  uint32_t mine = 0;  // <= tile/256 spans")
+    b = src.index("  atomicAdd(&sum, (unsigned long long)mine);")
+    old = src[a:b]
+    new = old.replace(
+        "  for (uint64_t i0 = lo; i0 < hi; i0 += kPlanThreads) {\n    const uint64_t i = i0 + threadIdx.x;\n",
+        f"  for (uint64_t i00 = lo; i00 < hi; i00 += {U}u * kPlanThreads) {{\n"
+        f"  uint64_t doff[{U}];\n  uint32_t dlen[{U}], dinit[{U}];\n"
+        f"#pragma unroll\n  for (uint32_t u = 0; u < {U}u; ++u) {{\n"
+        "    const uint64_t i = i00 + u * kPlanThreads + threadIdx.x;\n    doff[u] = 0;\n    dlen[u] = 0;\n    dinit[u] = 0;\n"
+        "    if (i < hi) {\n      const uint64_t q = a.idx != nullptr ? a.idx[i] : i;\n"
+        "      doff[u] = kDesc ? a.off[q] : q * a.stride;\n      dlen[u] = kDesc ? a.len[q] : a.len_c;\n"
+        "      dinit[u] = kDesc ? (a.init != nullptr ? a.init[q] : 0u) : a.init_c;\n    }\n  }\n"
+        f"#pragma unroll\n  for (uint32_t u = 0; u < {U}u; ++u) {{\n"
+        "    const uint64_t i0 = i00 + u * kPlanThreads;\n    const uint64_t i = i0 + threadIdx.x;\n")
+    new = new.replace("    const uint64_t q = a.idx != nullptr ? a.idx[i] : i;  // the caller's span\n"
+                      "    const uint64_t off = kDesc ? a.off[q] : q * a.stride;\n"
+                      "    const uint32_t len = kDesc ? a.len[q] : a.len_c;\n"
+                      "    const uint32_t init = kDesc ? (a.init != nullptr ? a.init[q] : 0u) : a.init_c;\n",
+                      "    const uint64_t off = doff[u];\n    const uint32_t len = dlen[u];\n    const uint32_t init = dinit[u];\n")
+    assert new.count("doff[u]") == 3 and new != old
+    new = new.rstrip("\n") + "\n  }\n"
+    return [("crc32c_kernels.hip", old, new)]
+
+
+VARIANTS["plan_x2"] = _plan_hoist(2)
+VARIANTS["plan_x4"] = _plan_hoist(4)
 # (trail_plain was adopted in 15de4d0 -- plain stores, four spans per thread,
 # variants trail_x1 / trail_nt there -- and reverted: its dirty lines cost the
 # next call more than the pass saved, profiles/r06/r06n_variants.json)
