@@ -305,7 +305,7 @@ void SyncAndRelease(Workspace& w) {
   {
     const char* t = reinterpret_cast<const char*>(t_last_counters);
     const char* c = reinterpret_cast<const char*>(w.ws.counters);
-    if (c != nullptr && t >= c && t < c + 512) t_last_counters = nullptr;
+    if (c != nullptr && t >= c && t < c + 2 * prismdb::dev::kCounterBlock) t_last_counters = nullptr;
   }
   if (w.direct != nullptr && t_last_stats == reinterpret_cast<const uint32_t*>(w.direct + 32)) t_last_stats = nullptr;
   int cur = 0;
@@ -382,13 +382,13 @@ int InitWorkspace(Workspace& w, int device, hipStream_t s) {
   w.device = device;
   w.stream = s;
   hipError_t e = hipSuccess;
-  const size_t bytes = 512 + kCapSeg * (16 + 4) + (size_t)kCapLong * (8 + 8 + 4) +
+  const size_t bytes = 2 * prismdb::dev::kCounterBlock + kCapSeg * (16 + 4) + (size_t)kCapLong * (8 + 8 + 4) +
                        (size_t)prismdb::dev::kMaxPlanBlocks * 8;
   e = hipEventCreateWithFlags(&w.done[0], hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&w.done[1], hipEventDisableTiming);
   if (e == hipSuccess) e = hipMallocAsync(&w.mem, bytes, s);
   // both planner counter blocks start zeroed (then each call zeroes the next's)
-  if (e == hipSuccess) e = hipMemsetAsync(w.mem, 0, 512, s);
+  if (e == hipSuccess) e = hipMemsetAsync(w.mem, 0, 2 * prismdb::dev::kCounterBlock, s);
   if (e != hipSuccess) {
     for (hipEvent_t ev : w.done)
       if (ev != nullptr) (void)hipEventDestroy(ev);
@@ -396,8 +396,8 @@ int InitWorkspace(Workspace& w, int device, hipStream_t s) {
     return FailHip(e, "workspace allocation");
   }
   char* p = static_cast<char*>(w.mem);
-  w.ws.counters = reinterpret_cast<SplitCounters*>(p);  // two 256-B blocks, one per call parity
-  p += 512;
+  w.ws.counters = reinterpret_cast<SplitCounters*>(p);  // two counter blocks, one per call parity
+  p += 2 * prismdb::dev::kCounterBlock;
   w.ws.seg_rec = reinterpret_cast<prismdb::dev::SpanRec*>(p);
   p += kCapSeg * 16;
   w.ws.long_span = reinterpret_cast<uint64_t*>(p);
@@ -706,15 +706,15 @@ int RunBatch(DeviceCtx& ctx, const SpanBatch& base_args, bool desc, bool verify,
   // planner call's plan kernel (or at the workspace's creation) -- no fill
   // kernel in front of the call (it and its gap took 6.7 us of a config-5
   // call, profiles/r05/r05aa_c5_seal/one_call_timeline.csv).
-  static_assert(sizeof(SplitCounters) <= 256, "each call parity's counter block is 256 B");
+  static_assert(sizeof(SplitCounters) <= 256, "SplitCounters fills the first 256 B of a counter block");
   {
     char* const cb = reinterpret_cast<char*>(w->ws.counters);
-    ws.counters = reinterpret_cast<SplitCounters*>(cb + 256u * (w->pcall & 1u));
-    ws.zero_next = reinterpret_cast<SplitCounters*>(cb + 256u * ((w->pcall + 1u) & 1u));
+    ws.counters = reinterpret_cast<SplitCounters*>(cb + prismdb::dev::kCounterBlock * (w->pcall & 1u));
+    ws.zero_next = reinterpret_cast<SplitCounters*>(cb + prismdb::dev::kCounterBlock * ((w->pcall + 1u) & 1u));
   }
   hipError_t e = hipSuccess;
   if (w->dirty) {  // the last call failed after using this block, before its plan kernel
-    e = hipMemsetAsync(ws.counters, 0, 256, s);
+    e = hipMemsetAsync(ws.counters, 0, prismdb::dev::kCounterBlock, s);
     if (e != hipSuccess) return FailHip(e, "hipMemsetAsync");
   }
   w->dirty = true;  // until this call's plan kernel is enqueued
@@ -772,23 +772,40 @@ int RunBatch(DeviceCtx& ctx, const SpanBatch& base_args, bool desc, bool verify,
   a.overflow = &ws.counters->overflow;
   a.rec = ws.rec;
   // The segment pass (long spans' 32 KiB pieces) needs only the plan: it
-  // runs on the workspace's side stream next to the span kernel, and takes
-  // CUs as the span kernel's groups leave them (~100 us of an SST-descriptor
-  // call ran after it before).  The combine waits for both.  The fork is the
-  // stop event of the last kernel before the span kernel (the slice mark, or
-  // the plan), not a marker after it: a marker there held the span kernel
-  // back ~6.5 us (profiles/r05/r05aa_c5_seal/one_call_timeline.csv).
+  // runs on the workspace's side stream from the plan kernel's end (the
+  // fork: that kernel's stop event, not a marker after it -- a marker held
+  // the next kernel back ~6.5 us, profiles/r05/r05aa_c5_seal), next to the
+  // slice kernels and the span kernel, whose groups take the CUs as its
+  // groups leave them.  The combine waits for both.  (Forked after the slice
+  // mark, it got CUs only as span-kernel groups left: once the pair-run
+  // kernel's tail balanced its waves they all left together, and a config-5
+  // call's 2145 segments ran after it, 30-140 us; profiles/r06/r06ag.)
   if ((rc = SideStream(w)) != 0) return rc;
   // Task-balanced slices need more records than span streams: with n <= the
   // stream count every stream holds at most one record either way, and the
   // two slice kernels' launches are ~9 us of a file-sized call.
   const bool sliced = a.n > streams;
-  e = prismdb::dev::launch_plan(a, desc, ws, s, sliced ? nullptr : w->fork);
+  e = prismdb::dev::launch_plan(a, desc, ws, s, w->fork);
   if (e != hipSuccess) return FailHip(e, "plan kernel launch");
   w->pcall++;  // the next call's block is the one this plan kernel zeroes
   w->dirty = false;
+  e = hipStreamWaitEvent(w->side, w->fork, 0);
+  if (e != hipSuccess) return FailHip(e, "side stream fork");
+  side_join.armed = true;
+  SpanBatch seg{};
+  seg.base = a.base;
+  seg.n = ws.cap_seg;
+  seg.n_dev = &ws.counters->nseg;
+  seg.out = ws.seg_out;
+  seg.skip_above = 0xFFFFFFFFu;
+  seg.overflow = &ws.counters->overflow;
+  seg.role = prismdb::dev::kRoleSegments;
+  seg.tabs = ctx.tabs;
+  seg.rec = ws.seg_rec;
+  e = prismdb::dev::launch_span(seg, false, ctx.cus, w->side, w->join);  // the join: its stop event
+  if (e != hipSuccess) return FailHip(e, "segment kernel launch");
   if (sliced) {
-    e = prismdb::dev::launch_slices(a, ws, s, w->fork);
+    e = prismdb::dev::launch_slices(a, ws, s);
     if (e != hipSuccess) return FailHip(e, "slice kernels launch");
     a.slice_start = ws.slice_start;
     a.nslices_dev = &ws.counters->nslices;
@@ -803,23 +820,9 @@ int RunBatch(DeviceCtx& ctx, const SpanBatch& base_args, bool desc, bool verify,
                       : 0u;
   t_last_pair = a.pair_kernel != 0u;
   a.claim = &ws.counters->claim;  // (zeroed with the counters above)
-  e = hipStreamWaitEvent(w->side, w->fork, 0);
-  if (e != hipSuccess) return FailHip(e, "side stream fork");
-  side_join.armed = true;
+  a.claims = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(ws.counters) + 256);
   e = prismdb::dev::launch_span(a, verify, ctx.cus, s);
   if (e != hipSuccess) return FailHip(e, "span kernel launch");
-  SpanBatch seg{};
-  seg.base = a.base;
-  seg.n = ws.cap_seg;
-  seg.n_dev = &ws.counters->nseg;
-  seg.out = ws.seg_out;
-  seg.skip_above = 0xFFFFFFFFu;
-  seg.overflow = &ws.counters->overflow;
-  seg.role = prismdb::dev::kRoleSegments;
-  seg.tabs = ctx.tabs;
-  seg.rec = ws.seg_rec;
-  e = prismdb::dev::launch_span(seg, false, ctx.cus, w->side, w->join);  // the join: its stop event
-  if (e != hipSuccess) return FailHip(e, "segment kernel launch");
   // The call's last kernel completes the workspace's done event itself (its
   // stop event) instead of a marker after it (MarkDone, on an error return).
   hipEvent_t const done = w->done[w->gen & 1u];
@@ -1114,18 +1117,22 @@ int prismdb_crc32c_last_schedule(uint64_t out[3]) {
 }
 
 // Test hook: the claimed tails of this thread's last planner-path batch:
-// out[0] = claims on the span / pair-run kernel's counter (slices or runs
+// out[0] = claims on the span / pair-run kernels' counters (slices or runs
 // taken on demand past the static deal, plus one failed claim per stream at
 // the end; 0 when the batch was too small for a tail), out[1] = the same for
 // the lane kernel's runs.  -2 after a one-launch batch, -1 before any.
 int prismdb_crc32c_last_claims(uint64_t out[2]) {
   if (t_last_direct) return -2;
   if (t_last_counters == nullptr || LastBatchStale()) return -1;
-  prismdb::dev::SplitCounters c{};
+  namespace d = prismdb::dev;
+  uint32_t blk[d::kCounterBlock / 4];
   hipError_t e = hipStreamSynchronize(t_last_stream);
-  if (e == hipSuccess) e = hipMemcpy(&c, t_last_counters, sizeof(c), hipMemcpyDeviceToHost);
+  if (e == hipSuccess) e = hipMemcpy(blk, t_last_counters, sizeof(blk), hipMemcpyDeviceToHost);
   if (e != hipSuccess) return FailHip(e, "prismdb_crc32c_last_claims");
-  out[0] = c.claim;
+  d::SplitCounters c{};
+  std::memcpy(&c, blk, sizeof(c));
+  out[0] = c.claim;  // the span kernel's, plus the pair-run kernel's claim lines
+  for (uint32_t j = 0; j < d::kClaimLines; ++j) out[0] += blk[64 + d::kClaimLineWords * j];
   out[1] = c.lane_claim;
   return 0;
 }

@@ -104,6 +104,9 @@ struct SpanBatch {
   // the lane kernel's for its last rounds of runs
   uint32_t* claim;
   const unsigned long long* tasks_dev;  // nullable: the span pass's chunk tasks (slice scan)
+  // nullable, zero at launch: the pair-run kernel's kClaimLines claim
+  // counters, one per 128-B line (word kClaimLineWords * j)
+  uint32_t* claims;
 };
 
 // Below this many spans the pair-run kernel's extra launch (~5 us) costs more
@@ -121,6 +124,14 @@ struct SplitCounters {
   uint32_t claim;                       // span kernel: tail slices claimed (SpanBatch::claim)
   uint32_t lane_claim;                  // lane kernel: tail runs claimed (its SpanBatch::claim)
 };
+
+// A planner call's counter block (two, by call parity): SplitCounters, then
+// the pair-run kernel's claim counters, one per 128-B line -- eight
+// counters, each taking the claims of an eighth of the groups (one address
+// took every wave's claim at ~86 per us: too few for config 5's short runs).
+constexpr uint32_t kClaimLines = 8;
+constexpr uint32_t kClaimLineWords = 32;
+constexpr uint32_t kCounterBlock = 256 + kClaimLines * 4 * kClaimLineWords;  // bytes
 
 struct SplitWs {
   SplitCounters* counters;

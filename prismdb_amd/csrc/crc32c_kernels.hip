@@ -584,14 +584,48 @@ __global__ __launch_bounds__(kThreads) void crc32c_pair_kernel(SpanBatch a) {
   set_prio();
 
   // Issue-side cursor: run k = [lo, hi) records, pair i of it.  Runs past
-  // Kst (the last kTailRounds rounds) are claimed on demand, as in
-  // crc32c_span_kernel (runs are never empty).
-  const uint32_t ptail = rq >= 31u ? kPairTailRounds : (rq >= 16u ? kPairTailRounds * rq / 31u : 0u);  // (the span kernel's note)
-  const uint32_t Kst = a.claim != nullptr && K > ptail * nwaves ? K - ptail * nwaves : K;
-  auto claim_run = [&]() -> uint32_t {
-    uint32_t got = 0;
-    if (lane == 0u) got = __hip_atomic_fetch_add(a.claim, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return Kst + rfl(got);
+  // Kst (the last kPairTailRounds rounds) are claimed on demand, as in
+  // crc32c_span_kernel (runs are never empty) -- but a claim's atomic goes
+  // out when the wave starts the run before it, and its return is read at
+  // that run's end: no wave waits for a claim.  (Read right away, each claim
+  // drained the wave's ring -- hipcc's vmcnt(0) -- and a tail cost short
+  // runs more than it balanced: 2.4 M SST spans at 4.6 pairs per run ran
+  // 20 % slower with 65 K claims, so batches under 16 pairs per run had
+  // none, and their waves left over 1505-1721 us of a 1.72 ms kernel, by
+  // SIMD age rank and XCD; profiles/r05/r05m, profiles/r06/r06ad_pair_waves.
+  // Prefetched claims on one counter balanced the waves but the counter took
+  // only ~86 claims per us against the ~170 per us config 5's short runs ask
+  // for: the kernel ran 20 % slower, r06ae_single_counter.  Eight counters:
+  // exits 1721-1756 us, desc4k -3.3 %, config-5 seals -2.4 %, r06af / r06ah.)
+  // The claim's return lands in lane 0 of a ring slot's edge register (lane
+  // 0 takes no edge byte: its load is out of range and returns 0 first), so
+  // no register is added to the ring and the ring's own counted wait for
+  // that slot retires it: issued right after a take's loads when the take
+  // starts a run whose successor is claimed, read after the slot's next wait
+  // -- two takes on, before that run's last take when runs hold >= 3 pairs
+  // (shorter runs: no tail).  tools/check_inflight.py audits the build (a
+  // claim register of its own, loop-carried, cost hipcc SGPR spills and
+  // failed the audit).
+  // Eight claim counters (kClaimLines), counter c for the groups b with
+  // (b / 8) % 8 == c (each set spans every XCD and holds every SIMD rank):
+  // counter c deals the tail runs Kst + c + 8 j.
+  const uint32_t ptail = rq >= 3u ? kPairTailRounds : 0u;
+  const uint32_t Kst = a.claims != nullptr && K > ptail * nwaves ? K - ptail * nwaves : K;
+  const uint32_t cset = (blockIdx.x >> 3) & (kClaimLines - 1u);
+  uint32_t* const ctr = a.claims != nullptr ? a.claims + kClaimLineWords * cset : nullptr;
+  auto claim_into = [&](uint32_t& e, uint32_t need) {
+    uint64_t sv;
+    asm volatile(
+        "s_cmp_eq_u32 %2, 0\n\t"
+        "s_cbranch_scc1 .Lno_claim%=\n\t"
+        "s_mov_b64 %1, exec\n\t"
+        "s_mov_b64 exec, 1\n\t"
+        "global_atomic_add %0, %3, %4, %5 sc0\n\t"
+        "s_mov_b64 exec, %1\n"
+        ".Lno_claim%=:"
+        : "+v"(e), "=&s"(sv)
+        : "s"(need), "v"(0u), "v"(1u), "s"(ctr)
+        : "memory", "scc");
   };
   uint32_t k = wave, lo = 0, hi = 0, i = 0;
   auto run_bounds = [&](uint32_t kk) {
@@ -599,8 +633,16 @@ __global__ __launch_bounds__(kThreads) void crc32c_pair_kernel(SpanBatch a) {
     hi = lo + 2u * (rq + (kk < rr ? 1u : 0u));
     hi = hi < n ? hi : n;
   };
-  if (k >= Kst && k < K) k = claim_run();
+  // the wave's next run after k is a claimed one
+  auto wants_claim = [&]() -> bool { return Kst < K && k < K && k + nwaves >= Kst; };
+  if (k >= Kst && k < K) {  // no static run: the first claim is waited for (no loads out yet)
+    uint32_t got = 0;
+    if (lane == 0u) got = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    k = Kst + cset + kClaimLines * rfl(got);
+  }
   if (k < K) run_bounds(k);
+  uint32_t kn = 0u;                  // the claimed successor of the current run, once read
+  uint32_t need = wants_claim() ? 1u : 0u;  // claim after this take's loads (the first: after take 0's)
   // b: the pair's first record (n: none left)
   auto pair_first = [&]() -> uint32_t { return k < K ? lo + 2u * i : n; };
   auto step = [&]() {
@@ -608,10 +650,10 @@ __global__ __launch_bounds__(kThreads) void crc32c_pair_kernel(SpanBatch a) {
     if (lo + 2u * (i + 1u) < hi) {
       ++i;
     } else {
-      k += nwaves;
+      k = wants_claim() ? kn : k + nwaves;  // (claimed: read two takes ago at the latest)
       i = 0;
-      if (k >= Kst && k < K + nwaves) k = claim_run();
       if (k < K) run_bounds(k);
+      need = wants_claim() ? 1u : 0u;
       prio = (prio + 1u) & 3u;
       set_prio();
     }
@@ -737,11 +779,15 @@ __global__ __launch_bounds__(kThreads) void crc32c_pair_kernel(SpanBatch a) {
     p0 = read_rec(pb);
     p1 = read_rec(pb + 1u);
   };
+  uint32_t cs[2];  // per slot: a claim rides in lane 0 of its edge register eb[sl][1]
 #pragma unroll
   for (int sl = 0; sl < 2; ++sl) {
     take(sl);
     issue(tk[sl][0], wb[sl][0], eb[sl][0]);
     issue(tk[sl][1], wb[sl][1], eb[sl][1]);
+    cs[sl] = rfl(need);  // (rfl: an SGPR operand -- hipcc takes the flag for divergent)
+    claim_into(eb[sl][1], cs[sl]);
+    need = 0u;
   }
   constexpr int kYounger = 2 * (kRounds + 1);  // the other slot's two spans
   for (;;) {
@@ -749,12 +795,16 @@ __global__ __launch_bounds__(kThreads) void crc32c_pair_kernel(SpanBatch a) {
     for (int sl = 0; sl < 2; ++sl) {
       wait_task<kYounger>(wb[sl][0], eb[sl][0]);
       wait_task<kYounger>(wb[sl][1], eb[sl][1]);
+      if (cs[sl] != 0u) kn = Kst + cset + kClaimLines * readlane(eb[sl][1], 0);
       if (tk[sl][0].valid())
         fold(tk[sl][0], wb[sl][0], eb[sl][0], tk[sl][1], wb[sl][1], eb[sl][1], tfirst[sl], tcnt[sl], tlast[sl] != 0u);
       if (!tk[sl ^ 1][0].valid()) goto drained;
       take(sl);
       issue(tk[sl][0], wb[sl][0], eb[sl][0]);
       issue(tk[sl][1], wb[sl][1], eb[sl][1]);
+      cs[sl] = rfl(need);
+      claim_into(eb[sl][1], cs[sl]);
+      need = 0u;
     }
   }
 drained:
@@ -940,8 +990,11 @@ template <bool kDesc>
 __global__ __launch_bounds__(kPlanThreads) void crc32c_plan_kernel(SpanBatch a, SplitWs ws) {
   // the next call's counters (the other parity's block, idle since the call
   // before this one): zeroed here instead of by a fill kernel in front of it
-  if (blockIdx.x == 0u && threadIdx.x < 64u && ws.zero_next != nullptr)
-    reinterpret_cast<uint32_t*>(ws.zero_next)[threadIdx.x] = 0u;
+  if (blockIdx.x == 0u && ws.zero_next != nullptr) {
+    uint32_t* const z = reinterpret_cast<uint32_t*>(ws.zero_next);
+    if (threadIdx.x < 64u) z[threadIdx.x] = 0u;  // SplitCounters
+    else if (threadIdx.x < 64u + kClaimLines) z[64u + kClaimLineWords * (threadIdx.x - 64u)] = 0u;  // claim lines
+  }
   const uint64_t n = batch_n(a);
   const uint64_t lo = (uint64_t)blockIdx.x * ws.tile;
   if (lo >= n) {  // (behind the lane kernel the list is often empty: ~4000 blocks leave at once)

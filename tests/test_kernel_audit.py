@@ -42,6 +42,23 @@ def test_inflight_audit_catches_an_injected_read(tmp_path):
     assert r.returncode == 1 and "in-flight [10]" in r.stdout, r.stdout
 
 
+def test_inflight_audit_tracks_asm_atomic_returns(tmp_path):
+    """An asm atomic with return (sc0) is in flight like a load: a copy of its
+    destination before a wait that retires it is reported, a read after is not."""
+    def run(lines):
+        f = tmp_path / "k.s"
+        f.write_text("\n".join(["k:"] + lines + ["\ts_endpgm"]) + "\n")
+        return subprocess.run([sys.executable, os.path.join(ROOT, "tools", "check_inflight.py"), str(f)],
+                              capture_output=True, text=True)
+    atomic = ["\t;;#ASMSTART", "\tglobal_atomic_add v12, v1, v2, s[4:5] sc0", "\t;;#ASMEND"]
+    load = ["\t;;#ASMSTART", "\tglobal_load_dword v10, v1, s[2:3] offset:0 nt", "\t;;#ASMEND"]
+    wait = ["\t;;#ASMSTART", "\ts_waitcnt vmcnt(1)", "\t;;#ASMEND"]
+    bad = run(atomic + load + ["\tv_mov_b32_e32 v11, v12"] + wait)
+    assert bad.returncode == 1 and "in-flight [12]" in bad.stdout, bad.stdout
+    good = run(atomic + load + wait + ["\tv_readfirstlane_b32 s6, v12", "\ts_waitcnt vmcnt(0)"])
+    assert good.returncode == 0, good.stdout
+
+
 def test_hazard_audit_catches_valu_sgpr_write(tmp_path):
     """v_readfirstlane into a descriptor SGPR right before an asm buffer load is reported."""
     asm = "\n".join([

@@ -10,7 +10,8 @@ fall-through) with a forward dataflow over "possibly in-flight" registers:
 
   * every vector-memory instruction (asm or not, loads and stores: they share
     vmcnt) ages the in-flight entries by one;
-  * an asm load adds its destination registers at age 0;
+  * an asm load (or an asm atomic with return, sc0) adds its destination
+    registers at age 0;
   * `s_waitcnt vmcnt(N)` (asm or compiler) retires entries of age >= N;
   * ages are capped at 64 (vmcnt holds at most 63 outstanding operations);
   * at a join the states are merged keeping each register's youngest age;
@@ -106,7 +107,9 @@ def step(state, inst, report=None):
         srcs |= dst
         if not op.startswith("v_writelane"):
             dst = set()
-    if report is not None and not (asm and is_vmem and op.find("load") >= 0 and not (srcs & set(state))):
+    # an asm atomic with return (sc0) lands in its destination like a load
+    ret = asm and is_vmem and ("load" in op or ("atomic" in op and re.search(r"\bsc0\b", t) is not None))
+    if report is not None and not (ret and not (srcs & set(state))):
         hit = (srcs | dst) & set(state)
         if hit:
             report.append((ln, t, sorted(hit)))
@@ -117,7 +120,7 @@ def step(state, inst, report=None):
     if is_vmem:
         state = {r: min(a + 1, 64) for r, a in state.items()}
         state = {r: a for r, a in state.items() if a < 64}
-        if asm and "load" in op:
+        if ret:
             for r in dst:
                 state[r] = 0
     return state
