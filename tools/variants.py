@@ -611,8 +611,8 @@ def _plan_hoist(U):
 
 VARIANTS["plan_x2"] = _plan_hoist(2)
 VARIANTS["plan_x4"] = _plan_hoist(4)
-# the pair-run kernel's claimed tail: 8 / 24 rounds (product: 16)
-for _r in (8, 24):
+# the pair-run kernel's claimed tail: 8 / 24 / 32 rounds (product: 16)
+for _r in (8, 24, 32):
     VARIANTS[f"ptail{_r}"] = [("crc32c_kernels.hip", "constexpr uint32_t kPairTailRounds = 16;",
                                f"constexpr uint32_t kPairTailRounds = {_r};")]
 # (trail_plain was adopted in 15de4d0 -- plain stores, four spans per thread,
