@@ -615,6 +615,19 @@ VARIANTS["plan_x4"] = _plan_hoist(4)
 for _r in (8, 24, 32):
     VARIANTS[f"ptail{_r}"] = [("crc32c_kernels.hip", "constexpr uint32_t kPairTailRounds = 16;",
                                f"constexpr uint32_t kPairTailRounds = {_r};")]
+# the lane kernel's claimed tail on the eight claim lines (kClaimLines)
+# instead of one counter (claims still read at once)
+VARIANTS["lane8"] = [
+    ("crc32c_capi.hip", "    a.claim = &ws.counters->lane_claim;  // (zeroed with the counters above)\n",
+     "    a.claim = &ws.counters->lane_claim;  // (zeroed with the counters above)\n"
+     "    a.claims = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(ws.counters) + 256);\n"),
+    ("crc32c_kernels.hip",
+     "      if (lane == 0u) got = __hip_atomic_fetch_add(a.claim, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);\n"
+     "      nx = Rs + rfl(got);\n",
+     "      const uint32_t cset = (blockIdx.x >> 3) & (kClaimLines - 1u);\n"
+     "      if (lane == 0u) got = __hip_atomic_fetch_add(a.claims + kClaimLineWords * cset, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);\n"
+     "      nx = Rs + cset + kClaimLines * rfl(got);\n"),
+]
 # (trail_plain was adopted in 15de4d0 -- plain stores, four spans per thread,
 # variants trail_x1 / trail_nt there -- and reverted: its dirty lines cost the
 # next call more than the pass saved, profiles/r06/r06n_variants.json)
