@@ -1115,23 +1115,25 @@ def _last_claims(native):
     return list(arr)
 
 
-@pytest.mark.parametrize("kernel", ["pair", "span"])
+@pytest.mark.parametrize("kernel", ["pair", "pair_short", "span"])
 def test_claimed_tails_engage(dev, oracle, native, kernel):
     """Batches sized from the device's CU count so that the planner kernels'
-    claimed tails engage: the pair-run kernel (one-task spans, >= 16 pairs
-    per run: 64 B spans, ~2300 per wave) and the span kernel (task-balanced
-    slices of >= 32 tasks, 16 per stream: spans of 1-3 chunks, ~16 GiB).
-    The claim counter read back is > 0, and the results are bit-exact: every
-    span for the pair batch, a sample plus the ends (host-regenerated bytes)
-    for the span batch."""
+    claimed tails engage: the pair-run kernel (one-task spans: 64 B spans,
+    ~2300 per wave, ~18 pairs per run; pair_short: ~600 per wave, ~4.7 pairs
+    per run, config 5's shape, whose claims ride one run ahead on the eight
+    claim counters) and the span kernel (task-balanced slices of >= 32
+    tasks, 16 per stream: spans of 1-3 chunks, ~16 GiB).  The claims read
+    back are > 0, and the results are bit-exact: every span for the pair
+    batches, a sample plus the ends (host-regenerated bytes) for the span
+    batch."""
     import torch
     from prismdb_amd import crc32c
 
     cus = torch.cuda.get_device_properties(0).multi_processor_count
     nwaves = 16 * cus  # kWavesPerGroup, one group per CU
-    seed = 0x5EED0080 + (kernel == "span")
-    if kernel == "pair":
-        n = 2300 * nwaves  # np / (64 nwaves) ~ 18 pairs per run >= 16
+    seed = 0x5EED0080 + (kernel == "span") + 2 * (kernel == "pair_short")
+    if kernel in ("pair", "pair_short"):
+        n = (2300 if kernel == "pair" else 600) * nwaves  # np / (64 nwaves): ~18 / ~4.7 pairs per run
         off = np.arange(n, dtype=np.uint64) * 64 + 3
         lens = np.full(n, 61, dtype=np.uint32)
         host = oracle.synth(n * 64 + 64, seed)
@@ -1160,7 +1162,7 @@ def test_claimed_tails_engage(dev, oracle, native, kernel):
     finally:
         restore()
     got = _u32(out)
-    if kernel == "pair":
+    if kernel != "span":
         assert sched[1] == 0 and sched[2] == 1  # every record one task: the pair-run kernel's schedule
         want, _ = oracle.batch(host, off, lens, mask=True)
         np.testing.assert_array_equal(got, want)
