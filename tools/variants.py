@@ -628,6 +628,16 @@ VARIANTS["lane8"] = [
      "      if (lane == 0u) got = __hip_atomic_fetch_add(a.claims + kClaimLineWords * cset, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);\n"
      "      nx = Rs + cset + kClaimLines * rfl(got);\n"),
 ]
+# the span kernel's claimed tail on the eight claim lines (claims still read
+# at once): counter (group / 8) % 8 deals the tail slices Kst + c + 8 j
+VARIANTS["span8"] = [
+    ("crc32c_kernels.hip",
+     "        if (lane == 0u) got = __hip_atomic_fetch_add(a.claim, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);\n"
+     "        k = Kst + rfl(got);\n",
+     "        const uint32_t cset = (blockIdx.x >> 3) & (kClaimLines - 1u);\n"
+     "        if (lane == 0u) got = __hip_atomic_fetch_add(a.claims + kClaimLineWords * cset, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);\n"
+     "        k = Kst + cset + kClaimLines * rfl(got);\n"),
+]
 # (trail_plain was adopted in 15de4d0 -- plain stores, four spans per thread,
 # variants trail_x1 / trail_nt there -- and reverted: its dirty lines cost the
 # next call more than the pass saved, profiles/r06/r06n_variants.json)
