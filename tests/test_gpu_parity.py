@@ -1290,3 +1290,29 @@ def test_band_routing_by_caller_intent(dev, oracle, native):
     assert native.prismdb_crc32c_last_schedule(sched) == -2
     np.testing.assert_array_equal(_u32(out), raw)
     assert not mm.cpu().numpy().any()
+
+
+def test_pair_tail_claims_repeat_against_fixed_kernel(dev):
+    """Config 5's data blocks (2.4 M spans of 3988 B at stride 3992: the
+    pair-run kernel, ~4.7 pairs per run, its tail claimed one run ahead on
+    eight counters) ten times over: the claims deal the tail runs in a
+    different order every call, and every call's results equal the fixed
+    kernel's over the same blocks (an independent kernel; tools/claim_stress.py
+    runs the same at 60 calls plus sealed config-5 partitions)."""
+    import torch
+    from prismdb_amd import crc32c
+
+    n = 2404116
+    free, _ = torch.cuda.mem_get_info()
+    if free < n * 3992 + (2 << 30):
+        pytest.skip("not enough device memory")
+    buf = torch.empty(n * 3992 + 64, dtype=torch.uint8, device=dev)
+    crc32c.fill_synthetic(buf, 0x5EED0C5C)
+    want, _ = crc32c.batch_fixed(buf, 3992, 3988, n, mask=True)
+    d_off = torch.arange(n, dtype=torch.int64, device=dev) * 3992
+    d_len = torch.full((n,), 3988, dtype=torch.int32, device=dev)
+    for _ in range(10):
+        out, _ = crc32c.batch(buf, d_off, d_len, mask=True, check_bounds=False)
+        assert int((out != want).sum().item()) == 0
+    del buf, d_off, d_len, want, out
+    torch.cuda.empty_cache()
