@@ -101,8 +101,9 @@ int leveldb_crc32c_batch_fixed(const void* dev_base, size_t stride, size_t len, 
  * (dev_init may be NULL: all 0).  Any byte alignment, any length (< 4 GiB).
  * Long spans are split across many wavefronts and recombined on the device.
  * Routing: <= 2^17 spans one kernel launch (an SST file, a log file);
- * 2^17 < n <= 2^18 spans that seal (WRITE_TRAILER) or verify block trailers
- * (dev_mismatch != NULL), without LOG_HEADER, two such launches (a
+ * batches that seal (WRITE_TRAILER) or verify block trailers (dev_mismatch
+ * != NULL), without LOG_HEADER: one launch up to 196 608 spans (11 SST files
+ * of 64 MiB, on a 256-CU device) and two such launches up to 2^18 (a
  * compaction's dozen SST files: uniform blocks run faster that way);
  * everything else the planner path (task-balanced slices: plain checksum
  * batches of mixed span sizes, log records, any batch beyond 2^18 spans).

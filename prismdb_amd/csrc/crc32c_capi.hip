@@ -89,7 +89,7 @@ std::atomic<bool> g_force_generic{false};
 // path): 0 = log-record batches (PRISMDB_CRC32C_LOG_HEADER), 1 = all, -1 = none.
 std::atomic<int> g_lane_mode{0};
 // Descriptor batches of at most this many spans take the one-launch kernel.
-std::atomic<uint64_t> g_direct_max{prismdb::dev::kDirectMaxSpans};
+std::atomic<uint64_t> g_direct_max{prismdb::dev::kDirectPlainSpans};
 // The one-launch path's ticket capacity (tests shrink it to reach the
 // whole-span fallback) and its debug flags (DirectWs::dbg).
 std::atomic<uint32_t> g_direct_cap{prismdb::dev::kDirectTickets};
@@ -644,8 +644,15 @@ int RunBatch(DeviceCtx& ctx, const SpanBatch& base_args, bool desc, bool verify,
         (void)hipStreamSynchronize(w->side);
     }
   } side_join{w, s};
+  // One launch: <= direct_max spans (2^17), or, by default (wmode 2), a
+  // batch that seals or verifies block trailers (not log records) up to the
+  // kernel's capacity -- the SST-file batches the windows below would
+  // otherwise cut in two.
+  const int wmode = g_windows.load(std::memory_order_relaxed);
+  const bool block_trailers = verify || (a.flags & prismdb::dev::kFlagWriteTrailer) != 0;
+  const bool sst_batch = wmode == 2 && block_trailers && !(a.flags & prismdb::dev::kFlagLogHeader);
   const bool direct = desc && (route == kRouteDirect ||
-                               (route == kRouteAuto && a.n <= g_direct_max.load(std::memory_order_relaxed)));
+                               (route == kRouteAuto && (a.n <= g_direct_max.load(std::memory_order_relaxed) || sst_batch)));
   if (direct && a.n <= prismdb::dev::kDirectMaxSpans &&
       a.n <= 64ull * (uint64_t)ctx.cus * (prismdb::dev::kDirectThreads / 64)) {
     prismdb::dev::DirectWs d{};
@@ -668,8 +675,6 @@ int RunBatch(DeviceCtx& ctx, const SpanBatch& base_args, bool desc, bool verify,
   // KiB) ran at 57.5 % of the roofline as windows against 70.5 % on the
   // planner path (profiles/r06/r06s_configs.json, config3_band).
   const uint64_t wmax = g_direct_max.load(std::memory_order_relaxed);
-  const int wmode = g_windows.load(std::memory_order_relaxed);
-  const bool block_trailers = verify || (a.flags & prismdb::dev::kFlagWriteTrailer) != 0;
   if (desc && route == kRouteAuto && wmax > 0 && a.n > wmax &&
       (wmode == 1 || (wmode == 2 && a.n <= 2 * wmax && block_trailers)) && !(a.flags & prismdb::dev::kFlagLogHeader))
     return RunWindows(ctx, base_args, verify, s, wmax);

@@ -163,7 +163,14 @@ struct SplitWs {
 // (body <= 4 KiB) are dealt to the waves in static runs; longer spans are cut
 // into tickets of 2^lg chunks that any wave may claim, and the wave that
 // finishes a span's last ticket combines the partial registers.
-constexpr uint64_t kDirectMaxSpans = 1ull << 17;
+// Capacity: 64 spans per wave's static run at 12 waves x 256 CUs (host-
+// checked against the device's own CU count).  The default routing sends
+// plain batches here only up to kDirectPlainSpans; batches that seal or
+// verify block trailers (SST files) up to the capacity: 8-10 SST files per
+// call ran 2-16 % faster in one launch than as two windows
+// (tools/files_per_call.py, profiles/r06/r06as_files_per_call.json).
+constexpr uint64_t kDirectMaxSpans = 196608ull;
+constexpr uint64_t kDirectPlainSpans = 1ull << 17;
 constexpr int kDirectThreads = 768;  // per group, one group per CU: a wave's static run is <= 64 spans
                                      // while n <= 64 * 8 * CUs (host-checked)
 constexpr uint32_t kDirectTickets = 1u << 19;  // tickets per workspace slot (beyond: whole spans, one wave each)

@@ -1262,9 +1262,10 @@ def test_lane_runs_without_owned_records(dev, oracle, native, layout):
 
 def test_band_routing_by_caller_intent(dev, oracle, native):
     """2^17 < n <= 2^18 spans with the default routing: a plain checksum batch
-    takes the planner path, the same spans sealed or verified take two
-    windows of the one-launch kernel (include/prismdb_crc32c.h); bit-exact on
-    every route."""
+    takes the planner path, the same spans sealed or verified take the
+    one-launch kernel (one launch up to its 196 608-span capacity, as these
+    150 000; two windows above: include/prismdb_crc32c.h); bit-exact on every
+    route."""
     import torch
     from prismdb_amd import crc32c
 
@@ -1283,7 +1284,7 @@ def test_band_routing_by_caller_intent(dev, oracle, native):
     assert native.prismdb_crc32c_last_schedule(sched) == 0  # the planner path
     np.testing.assert_array_equal(_u32(out), raw)
     out, _ = crc32c.batch(buf, d_off, d_len, mask=True, trailer=True)
-    assert native.prismdb_crc32c_last_schedule(sched) == -2  # windows of the one-launch kernel
+    assert native.prismdb_crc32c_last_schedule(sched) == -2  # the one-launch kernel
     masked = np.array([oracle.mask(int(c)) for c in raw], dtype=np.uint32)
     np.testing.assert_array_equal(_u32(out), masked)
     out, mm = crc32c.batch(buf, d_off, d_len, verify=True)

@@ -147,15 +147,17 @@ def test_full_sst_seal_reproduces_file(dev, native, table):
     assert buf.cpu().numpy().tobytes() == img
 
 
-@pytest.mark.parametrize("copies,route", [(7, "direct"), (12, "windows"), (12, "planner")])
+@pytest.mark.parametrize("copies,route", [(7, "direct"), (10, "direct"), (12, "windows"), (12, "planner")])
 def test_full_sst_copies_per_call(dev, native, table, copies, route):
     """A compaction's worth of reference tables per call: `copies` copies of
     the file back to back (16-B aligned), sealed from zeroed crcs in one call
     (byte-identical to the copies of the reference file), then verified in
     one call with one damaged data block per copy (exactly those flagged).
-    7 copies take one launch of the one-launch kernel; 12 copies (~201 K
-    spans) take its windows (the default up to 2^18 spans) or, pinned, the
-    planner path."""
+    7 and 10 copies (~168 K spans: past 2^17, within the one-launch
+    kernel's 196 608-span capacity, which batches sealing or verifying
+    block trailers use) take one launch of the one-launch kernel; 12 copies
+    (~201 K spans) take its windows (the default up to 2^18 spans) or,
+    pinned, the planner path."""
     import torch
     from prismdb_amd import crc32c
 

@@ -638,6 +638,11 @@ VARIANTS["span8"] = [
      "        if (lane == 0u) got = __hip_atomic_fetch_add(a.claims + kClaimLineWords * cset, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);\n"
      "        k = Kst + cset + kClaimLines * rfl(got);\n"),
 ]
+# the one-launch limit raised from 2^17 spans to 196 608 (64 spans per wave
+# at 12 waves x 256 CUs): 8-11 SST files per call in one launch instead of
+# two windows (tools/files_per_call.py)
+VARIANTS["direct196k"] = [("crc32c_device.h", "constexpr uint64_t kDirectMaxSpans = 1ull << 17;",
+                           "constexpr uint64_t kDirectMaxSpans = 196608ull;")]
 # (trail_plain was adopted in 15de4d0 -- plain stores, four spans per thread,
 # variants trail_x1 / trail_nt there -- and reverted: its dirty lines cost the
 # next call more than the pass saved, profiles/r06/r06n_variants.json)
