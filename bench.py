@@ -85,9 +85,10 @@ def parse():
     # (20, as the headline's steps: at 5 the first call's launch latency and
     # the closing synchronisation were ~1.5 % of a one-process config-5 round)
     ap.add_argument("--c5-steps", type=int, default=20)
-    ap.add_argument("--c5-files-per-call", default="7,12",
+    ap.add_argument("--c5-files-per-call", default="7,11,12",
                     help="config-5 compaction legs: SST files per leveldb_crc32c_batch call (comma list; 7 files "
-                         "are the most one launch takes, 12 a compaction's input set: 1 file + ~11 overlapping)")
+                         "are the most one launch takes below 2^17 spans, 11 the most a sealing or verifying batch "
+                         "takes in one launch on 256 CUs, 12 a compaction's input set: 1 file + ~11 overlapping)")
     ap.add_argument("--no-multi", action="store_true", help="skip the one-process batch_multi leg")
     ap.add_argument("--multi-timeout", type=float, default=240.0,
                     help="seconds the batch_multi leg's child process may take before it is stopped")
